@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Headline benchmark: gossip edge-deliveries/s (GTEPS) on a 2^24-node Chung-Lu
+power-law overlay (gamma 2.5, mean degree 16) with 4096 concurrent messages
+(BASELINE.json config 4), plus the HBM roofline fraction of the expansion kernel.
+
+One step = one complete gossip run: reset the Message-Lists, inject all 4096
+messages at their origins (round 0), and run forward-once rounds until no vertex
+receives anything new.  value = protocol edge-deliveries (sum of `sends` over all
+rounds = 4096 x arcs for a connected overlay) / wall time of the timed steps.
+
+python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 is launched by
+torch.distributed.run (one process per GPU; the data path is RCCL inside
+libgossip_hip.so, torch.distributed/gloo only distributes the RCCL id and the
+timings).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--log2n", type=int, default=24)
+    ap.add_argument("--dbar", type=float, default=16.0)
+    ap.add_argument("--gamma", type=float, default=2.5)
+    ap.add_argument("--messages", type=int, default=4096)
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--hub-threshold", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-messages", type=int, default=64)
+    ap.add_argument("--profile-steps", action="store_true",
+                    help="print per-round stats of the last step to stderr")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def allmax(pg, x):
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def round_bytes(st, words, nloc):
+    """Algorithmic bytes of one expansion launch of the sparse-aware pull
+    (DESIGN.md §4): per owned vertex 21 B of vertex state, per scanned arc 8 B
+    (column id + the neighbour's frontier popcount), per gathered frontier row
+    8W B, per receiver seen row read 8W B, per written row 16W B (next + seen)."""
+    w8 = 8 * words
+    return (21 * nloc + 8 * st["arcs_scanned"] + w8 * (st["rows_gathered"] + st["seen_rows_read"])
+            + 2 * w8 * st["rows_written"])
+
+
+def dense_round_bytes(n, nnz, words):
+    """SURVEY.md §8d dense-pull formula (for reference only)."""
+    return 8 * (n + 1) + 4 * nnz + 8 * words * nnz + 24 * words * n
+
+
+def cpu_baseline(args, eng, origin, pkg):
+    """The CPU oracle (oracle/gossip_oracle.c, OpenMP) on the same overlay with the
+    first `cpu_messages` of the 4096 messages (one 64-bit word per vertex): a
+    bounded sample of the same workload, in the same unit."""
+    from oracle import lib as oracle_lib
+    g = eng.graph()
+    threads = args.cpu_threads or min(os.cpu_count() or 1, 16)
+    o = origin[:args.cpu_messages]
+    t0 = time.perf_counter()
+    ref = oracle_lib.run(g, o, nthreads=threads, want_forwards=False)
+    dt = time.perf_counter() - t0
+    sends = sum(s["sends"] for s in ref["stats"])
+    return {"value": sends / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
+            "sample": f"oracle/gossip_oracle.c, same 2^{args.log2n}-node overlay, first "
+                      f"{len(o)} of {args.messages} messages, full run ({ref['rounds']} rounds, "
+                      f"{sends} edge-deliveries, {dt:.1f} s, {threads} OpenMP threads)"}
+
+
+def main():
+    args = parse()
+    world, rank, local, pg = dist_setup(args)
+    import _gossip_pkg
+    pkg = _gossip_pkg.load()
+    n = 1 << args.log2n
+    eng = pkg.GossipEngine(local, track_digest=1, track_first=0, hub_threshold=args.hub_threshold)
+    t0 = time.perf_counter()
+    eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
+    _, nnz, _, _ = eng.info()
+    if world > 1:
+        eng.set_partition(rank, world)
+        uid = [pkg.GossipEngine.comm_unique_id() if rank == 0 else None]
+        pg.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0], world, rank)
+    origin = pkg.overlay.random_origins(n, args.messages, seed=args.seed)
+    eng.set_messages(origin)
+    setup_s = time.perf_counter() - t0
+    vb, ve = eng.partition()
+
+    def step():
+        eng.reset()
+        return eng.run()
+
+    for _ in range(args.warmup):
+        step()
+    barrier(pg)
+    eng.synchronize()
+    t0 = time.perf_counter()
+    runs = [step() for _ in range(args.steps)]
+    eng.synchronize()
+    barrier(pg)
+    dt = allmax(pg, time.perf_counter() - t0)
+
+    sends = sum(s["sends"] for r in runs for s in r)   # global (all-reduced) counters
+    rounds = sum(len(r) for r in runs)
+    exp_ms = sum(s["expand_ms"] for r in runs for s in r)
+    exch_ms = sum(s["exchange_ms"] for r in runs for s in r)
+    nbytes = sum(round_bytes(s, eng.words, ve - vb) for r in runs for s in r)
+    if world > 1:   # byte counters are global: per-rank share for the per-GPU roofline
+        nbytes /= world
+    achieved = nbytes / (exp_ms * 1e-3) / 1e9 if exp_ms > 0 else 0.0
+    dense_eq = dense_round_bytes(n, nnz, eng.words) * rounds / world / (exp_ms * 1e-3) / 1e9
+    if args.profile_steps and rank == 0:
+        for s in runs[-1]:
+            print(json.dumps({k: s[k] for k in ("round", "new_bits", "sends", "active", "receivers",
+                                                "arcs_scanned", "rows_gathered", "seen_rows_read",
+                                                "rows_written", "expand_ms", "exchange_ms")}),
+                  file=sys.stderr)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, eng, origin, pkg)
+    if rank == 0:
+        out = {
+            "metric": "gossip edge-deliveries/s (GTEPS) & HBM roofline %, 2^24 nodes x 4096 msgs",
+            "value": sends / dt / 1e9,
+            "unit": "GTEPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (device-built Chung-Lu overlay, seeded origins)",
+            "config": {"workload": "C4: Chung-Lu gamma=2.5 overlay, full forward-once gossip run",
+                       "n": n, "arcs": nnz, "mean_degree": nnz / n, "messages": args.messages,
+                       "words_per_row": eng.words, "rounds_per_step": rounds / args.steps,
+                       "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,
+                       "parallelism": f"vertex-partition x{world}" + (" (RCCL all-gather)" if world > 1 else ""),
+                       "setup_s": round(setup_s, 2)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": f"k_expand<{eng.words}> (+hub passes), HIP events on the engine stream",
+                         "avg_launch_ms": exp_ms / rounds,
+                         "alg_bytes_per_launch": nbytes / rounds,
+                         "dense_equivalent_GBs": dense_eq,
+                         "exchange_ms_per_round": exch_ms / rounds},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,61 @@
+"""Build libgossip_hip.so for gfx950 in-tree (csrc/ -> _build/).
+
+hipcc cross-compiles without a GPU, so this runs in the CPU container; the
+built .so travels to the GPU box with the repo snapshot.
+"""
+import os
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+OUT_DIR = os.path.join(PKG_DIR, "_build")
+LIB = os.path.join(OUT_DIR, "libgossip_hip.so")
+INCLUDE = os.path.join(os.path.dirname(PKG_DIR), "include", "gossip_capi.h")
+SOURCES = ["gossip_engine.hip", "graph_build.hip"]
+HEADERS = ["gp_common.h", "gp_internal.h"]
+ARCH = os.environ.get("GOSSIP_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", f"--offload-arch={ARCH}"]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    return "hipcc"
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=True):
+    os.makedirs(OUT_DIR, exist_ok=True)
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [INCLUDE, __file__]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objs, procs = [], []
+    for s in SOURCES:
+        obj = os.path.join(OUT_DIR, os.path.splitext(s)[0] + ".o")
+        objs.append(obj)
+        cmd = [_hipcc(), *FLAGS, "-c", os.path.join(CSRC, s), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("hipcc failed")
+    tmp = LIB + ".tmp"
+    cmd = [_hipcc(), *FLAGS, "-shared", *objs, "-o", tmp, "-lrccl"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,1480 @@
+// gossip_engine.hip -- MI355X (gfx950) gossip-propagation engine: round kernels
+// and the C-ABI of include/gossip_capi.h.
+//
+// One gossip round r over all peers at once:
+//   L_r  liveness: crash draws, heartbeat-miss counters, 3-miss detection,
+//        dead-node reports, seed removal      (Peer.py:298-393, Seed.py:358-406)
+//   I_r  injection of messages generated in round r     (Peer.py:395-400)
+//   E_r  pull expansion: next[v] = OR_{u in In(v)} frontier[u] & ~seen[v];
+//        seen |= next  (forward-once with the Message-List bitmap `seen`;
+//        the send loop is Peer.py:402-404, the receive side Peer.py:175-216)
+//   X_r  (multi-GPU) RCCL all-gather of the owned next rows + popcounts.
+//
+// Data layout in HBM (row = W uint64 words = 64*W messages of one vertex):
+//   frontier/next  u64[n_alloc][W]   rows whose fpop == 0 are never read
+//   fpop           u32[n_alloc]      |frontier(v)|, doubles as the row-valid flag
+//   seen           u64[nloc][W]      Message-List of the owned vertices
+//   seenpop        u32[nloc]         |seen(v)| -> vertices holding all m skip E_r
+//   in-CSR         i64 row_ptr[n+1], i32 col[nnz]
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gp_internal.h"
+
+namespace gp {
+
+static thread_local std::string g_err;
+int set_error(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+typedef unsigned long long u64;
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+
+constexpr int BLOCK = 256;         // 4 waves
+constexpr int WAVES = BLOCK / 64;
+constexpr int NPART = 2048;        // partial stat slots (spread the atomics)
+constexpr int NST = 16;            // stats kept per partial slot (slots 0..15)
+
+// ---------------------------------------------------------------------------
+// geometry: a wave loads 16 B per lane -> W/2 lanes per row, 128/W rows per
+// wave-instruction (W == 1: 8 B per lane, 64 rows per instruction)
+template <int W>
+struct Geo {
+  static constexpr int WPL = W >= 2 ? 2 : 1;   // words per lane
+  static constexpr int LPR = W / WPL;          // lanes per row
+  static constexpr int RPI = 64 / LPR;         // rows per wave-instruction
+};
+
+template <int W>
+__device__ __forceinline__ u64x2 load_piece(const u64* __restrict__ base, int64_t row, int lw) {
+  if constexpr (W >= 2) {
+    return *reinterpret_cast<const u64x2*>(base + row * W + lw * 2);
+  } else {
+    u64x2 r;
+    r.x = base[row];
+    r.y = 0;
+    return r;
+  }
+}
+template <int W>
+__device__ __forceinline__ void store_piece(u64* __restrict__ base, int64_t row, int lw, u64x2 x) {
+  if constexpr (W >= 2) {
+    *reinterpret_cast<u64x2*>(base + row * W + lw * 2) = x;
+  } else {
+    base[row] = x.x;
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) x += __shfl_xor(x, s);
+  return x;
+}
+__device__ __forceinline__ u64 wave_xor_u64(u64 x) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) x ^= __shfl_xor(x, s);
+  return x;
+}
+__device__ __forceinline__ int lane_rank(u64 mask) {  // set bits of mask below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// ---------------------------------------------------------------------------
+// per-wave counters, flushed once per block into one of NPART slots
+struct WaveStats {
+  u64 c[NST];
+};
+__device__ __forceinline__ void ws_zero(WaveStats& s) {
+#pragma unroll
+  for (int k = 0; k < NST; ++k) s.c[k] = 0;
+}
+__device__ void flush_stats(const WaveStats& s, u64* __restrict__ partial) {
+  __shared__ u64 red[WAVES][NST];
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NST; ++k) red[wib][k] = s.c[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < NST) {
+    u64 t = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) t += red[w][threadIdx.x];
+    if (t) atomicAdd(&partial[(size_t)(blockIdx.x % NPART) * NST + threadIdx.x], t);
+  }
+}
+__global__ void k_stats_reduce(u64* __restrict__ partial, u64* __restrict__ stats) {
+  // one block of 256 threads; thread t sums slot (t % NST) over a strided part
+  __shared__ u64 acc[BLOCK];
+  const int k = threadIdx.x % NST, lane_grp = threadIdx.x / NST;   // 16 groups
+  u64 t = 0;
+  for (int p = lane_grp; p < NPART; p += BLOCK / NST) {
+    t += partial[(size_t)p * NST + k];
+    partial[(size_t)p * NST + k] = 0;
+  }
+  acc[threadIdx.x] = t;
+  __syncthreads();
+  if (threadIdx.x < NST) {
+    u64 s = 0;
+    for (int g = 0; g < BLOCK / NST; ++g) s += acc[g * NST + threadIdx.x];
+    stats[threadIdx.x] += s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// expansion
+struct ExpandArgs {
+  const int64_t* __restrict__ row_ptr;
+  const int32_t* __restrict__ col;
+  const u64* __restrict__ front;       // frontier_r
+  const uint32_t* __restrict__ fpop;   // |frontier_r|
+  u64* __restrict__ next;
+  uint32_t* __restrict__ fpop_next;
+  u64* __restrict__ seen;
+  uint32_t* __restrict__ seenpop;
+  uint8_t* __restrict__ first;         // may be null
+  u64* __restrict__ digest;            // may be null
+  const uint8_t* __restrict__ state;
+  const int32_t* __restrict__ deg_live;
+  u64* __restrict__ partial;
+  const HubItem* __restrict__ hub_items;
+  const int32_t* __restrict__ hubs;
+  const int32_t* __restrict__ hub_item_ptr;
+  u64* __restrict__ hub_partial;
+  uint32_t* __restrict__ hub_pnz;
+  int64_t vbegin, nloc;
+  int64_t n_items;                     // hub items / hubs for the hub kernels
+  int32_t m_total;
+  int32_t rr;                          // receipt round of this expansion (r + 1)
+  int32_t hub_thr;
+  int32_t vpw;                         // vertices per wave (k_expand)
+};
+
+// OR the frontier rows of the active in-neighbours in arcs [b, e) into acc.
+// Neighbour ids are staged in LDS 64 at a time, compacted to the active ones.
+template <int W>
+__device__ __forceinline__ void gather(const ExpandArgs& a, int64_t b, int64_t e,
+                                       int32_t* __restrict__ sidx, int lane, int g, int lw,
+                                       u64x2& acc, WaveStats& st) {
+  constexpr int RPI = Geo<W>::RPI;
+  for (int64_t j0 = b; j0 < e; j0 += 64) {
+    const int n = (int)min((int64_t)64, e - j0);
+    int u = -1;
+    if (lane < n) u = a.col[j0 + lane];
+    const bool act = (u >= 0) && (a.fpop[u] != 0u);
+    const u64 mask = __ballot(act);
+    const int cnt = __popcll(mask);
+    st.c[S_ARCS] += n;
+    st.c[S_GATHERED] += cnt;
+    if (cnt == 0) continue;
+    if (act) sidx[lane_rank(mask)] = u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int k = g; k < cnt; k += 4 * RPI) {
+      const int k1 = k + RPI, k2 = k + 2 * RPI, k3 = k + 3 * RPI;
+      const int u0 = sidx[k];
+      const int u1 = k1 < cnt ? sidx[k1] : -1;
+      const int u2 = k2 < cnt ? sidx[k2] : -1;
+      const int u3 = k3 < cnt ? sidx[k3] : -1;
+      u64x2 r0 = load_piece<W>(a.front, u0, lw);
+      u64x2 r1 = {0, 0}, r2 = {0, 0}, r3 = {0, 0};
+      if (u1 >= 0) r1 = load_piece<W>(a.front, u1, lw);
+      if (u2 >= 0) r2 = load_piece<W>(a.front, u2, lw);
+      if (u3 >= 0) r3 = load_piece<W>(a.front, u3, lw);
+      acc |= (r0 | r1) | (r2 | r3);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// OR-reduce the row slots of the wave: afterwards every lane holds the full
+// result for its lw column.
+template <int W>
+__device__ __forceinline__ void reduce_slots(u64x2& acc) {
+  constexpr int LPR = Geo<W>::LPR;
+#pragma unroll
+  for (int s = LPR; s < 64; s <<= 1) {
+    acc.x |= __shfl_xor(acc.x, s);
+    if constexpr (W >= 2) acc.y |= __shfl_xor(acc.y, s);
+  }
+}
+
+__device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int word, u64 bits,
+                                                uint32_t rr) {
+  // row: first-receipt bytes of one vertex (stride W*64); 8-byte RMW per byte group
+  u64* p = reinterpret_cast<u64*>(row + (size_t)word * 64);
+  while (bits) {
+    const int grp = (__ffsll((long long)bits) - 1) >> 3;   // byte group of lowest set bit
+    const u64 gbits = (bits >> (grp * 8)) & 0xFFull;
+    u64 f = p[grp];
+    u64 m = gbits;
+    while (m) {
+      const int b = __ffsll((long long)m) - 1;
+      f = (f & ~(0xFFull << (8 * b))) | ((u64)rr << (8 * b));
+      m &= m - 1;
+    }
+    p[grp] = f;
+    bits &= ~(0xFFull << (grp * 8));
+  }
+}
+
+// receiver side of vertex v (local index i): apply seen, write next, counters
+template <int W>
+__device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
+                                           int g, int lw, WaveStats& st) {
+  constexpr int WPL = Geo<W>::WPL;
+  const bool nz = (acc.x | acc.y) != 0;
+  if (!__any(nz)) {
+    if (lane == 0) a.fpop_next[v] = 0;
+    return;
+  }
+  st.c[S_SEEN_READ] += 1;
+  u64x2 sv = {0, 0}, nw = {0, 0};
+  if (g == 0) {
+    sv = load_piece<W>(a.seen, i, lw);
+    nw = acc & ~sv;
+  }
+  const uint32_t pc = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
+  const uint32_t tot = wave_sum_u32(pc);
+  if (tot == 0) {
+    if (lane == 0) a.fpop_next[v] = 0;
+    return;
+  }
+  if (g == 0) {
+    store_piece<W>(a.next, v, lw, nw);
+    if (nw.x | nw.y) store_piece<W>(a.seen, i, lw, sv | nw);
+    if (a.first) {
+      uint8_t* row = a.first + (size_t)i * (W * 64);
+      if (nw.x) set_first_bytes(row, lw * WPL, nw.x, (uint32_t)a.rr);
+      if (WPL == 2 && nw.y) set_first_bytes(row, lw * WPL + 1, nw.y, (uint32_t)a.rr);
+    }
+  }
+  if (a.digest) {
+    u64 t = 0;
+    if (g == 0) {
+      if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(lw * WPL), nw.x);
+      if (WPL == 2 && nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(lw * WPL + 1), nw.y);
+    }
+    t = wave_xor_u64(t);
+    if (lane == 0) a.digest[i] ^= t;
+  }
+  if (lane == 0) {
+    a.fpop_next[v] = tot;
+    a.seenpop[i] += tot;
+  }
+  st.c[S_NEW_BITS] += tot;
+  st.c[S_RECEIVERS] += 1;
+  st.c[S_WRITTEN] += 1;
+}
+
+// main pull kernel: one wave per vertex, a.vpw consecutive vertices per wave
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
+  constexpr int LPR = Geo<W>::LPR;
+  __shared__ int32_t s_idx[WAVES][64];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  WaveStats st;
+  ws_zero(st);
+  const int64_t first_i = ((int64_t)blockIdx.x * WAVES + wib) * a.vpw;
+  const int64_t last_i = min(first_i + a.vpw, a.nloc);
+  for (int64_t i = first_i; i < last_i; ++i) {
+    const int v = (int)(a.vbegin + i);
+    const uint32_t fp = a.fpop[v];
+    if (fp) {
+      st.c[S_SENDS] += (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
+      st.c[S_ACTIVE] += 1;
+    }
+    if (a.state[v] & ST_DOWN) {
+      if (lane == 0) a.fpop_next[v] = 0;
+      continue;
+    }
+    if (a.seenpop[i] >= (uint32_t)a.m_total) {
+      if (lane == 0) a.fpop_next[v] = 0;
+      continue;
+    }
+    const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
+    if (e - b > a.hub_thr) continue;   // split over waves by the hub kernels
+    st.c[S_VISITED] += 1;
+    u64x2 acc = {0, 0};
+    gather<W>(a, b, e, s_idx[wib], lane, g, lw, acc, st);
+    reduce_slots<W>(acc);
+    finish_row<W>(a, v, i, acc, lane, g, lw, st);
+  }
+  flush_stats(st, a.partial);
+}
+
+// hubs, pass 1: one wave per (hub, arc chunk) -> partial OR row
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
+  constexpr int LPR = Geo<W>::LPR;
+  __shared__ int32_t s_idx[WAVES][64];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  WaveStats st;
+  ws_zero(st);
+  const int64_t it = (int64_t)blockIdx.x * WAVES + wib;
+  if (it < a.n_items) {
+    const HubItem h = a.hub_items[it];
+    const int64_t i = h.v - a.vbegin;
+    u64x2 acc = {0, 0};
+    if (!(a.state[h.v] & ST_DOWN) && a.seenpop[i] < (uint32_t)a.m_total) {
+      gather<W>(a, h.beg, h.end, s_idx[wib], lane, g, lw, acc, st);
+      reduce_slots<W>(acc);
+    }
+    const bool nz = __any((acc.x | acc.y) != 0);
+    if (nz && g == 0) store_piece<W>(a.hub_partial, it, lw, acc);
+    if (lane == 0) a.hub_pnz[it] = nz ? 1u : 0u;
+  }
+  flush_stats(st, a.partial);
+}
+
+// hubs, pass 2: one wave per hub -> OR the partials, then the receiver side
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
+  constexpr int LPR = Geo<W>::LPR;
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  WaveStats st;
+  ws_zero(st);
+  const int64_t h = (int64_t)blockIdx.x * WAVES + wib;
+  if (h < a.n_items) {
+    const int v = a.hubs[h];
+    const int64_t i = v - a.vbegin;
+    if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= (uint32_t)a.m_total) {
+      if (lane == 0) a.fpop_next[v] = 0;
+    } else {
+      st.c[S_VISITED] += 1;
+      u64x2 acc = {0, 0};
+      const int p0 = a.hub_item_ptr[h], p1 = a.hub_item_ptr[h + 1];
+      if (g == 0) {
+        for (int p = p0; p < p1; ++p)
+          if (a.hub_pnz[p]) acc |= load_piece<W>(a.hub_partial, p, lw);
+      }
+      finish_row<W>(a, v, i, acc, lane, g, lw, st);
+    }
+  }
+  flush_stats(st, a.partial);
+}
+
+// ---------------------------------------------------------------------------
+// injection (I_r): one wave per (round, origin) group.  Frontier rows are
+// replicated on every rank, so every rank applies every group; the owner of
+// the origin also updates its Message-List, first-receipt and counters.
+struct InjectArgs {
+  const int32_t* __restrict__ origin;
+  const u64* __restrict__ bits;
+  const uint32_t* __restrict__ cnt;
+  u64* __restrict__ front;
+  uint32_t* __restrict__ fpop;
+  u64* __restrict__ seen;
+  uint32_t* __restrict__ seenpop;
+  uint8_t* __restrict__ first;
+  u64* __restrict__ digest;
+  const uint8_t* __restrict__ state;
+  u64* __restrict__ partial;
+  int64_t off, groups;
+  int64_t vbegin, vend;
+  int32_t words;
+  int32_t r;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  WaveStats st;
+  ws_zero(st);
+  const int64_t k = (int64_t)blockIdx.x * WAVES + wib;
+  if (k < a.groups) {
+    const int64_t gi = a.off + k;
+    const int o = a.origin[gi];
+    const bool owned = o >= a.vbegin && o < a.vend;
+    if (a.state[o] & ST_DOWN) {
+      if (owned) st.c[S_LOST] += a.cnt[gi];
+    } else {
+      const uint32_t fp = a.fpop[o];
+      u64 b = 0, f = 0;
+      if (lane < a.words) {
+        b = a.bits[gi * a.words + lane];
+        f = fp ? a.front[(size_t)o * a.words + lane] : 0ull;
+        f |= b;
+        a.front[(size_t)o * a.words + lane] = f;
+      }
+      const uint32_t tot = wave_sum_u32((uint32_t)__popcll(f));
+      if (lane == 0) a.fpop[o] = tot;
+      if (owned) {
+        const int64_t i = o - a.vbegin;
+        if (lane < a.words) {
+          a.seen[i * a.words + lane] |= b;
+          if (a.first && b) set_first_bytes(a.first + (size_t)i * a.words * 64, lane, b, (uint32_t)a.r);
+        }
+        const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
+        if (a.digest) {
+          u64 t = b ? digest_term((uint32_t)a.r, (uint32_t)lane | DIGEST_INJECT, b) : 0ull;
+          t = wave_xor_u64(t);
+          if (lane == 0) a.digest[i] ^= t;
+        }
+        if (lane == 0) a.seenpop[i] += nb;
+        st.c[S_INJECTED] += a.cnt[gi];
+      }
+    }
+  }
+  flush_stats(st, a.partial);
+}
+
+// ---------------------------------------------------------------------------
+// liveness (L_r).  Replicated on every rank (deterministic), counters and
+// reports only for owned vertices.
+struct LiveArgs {
+  uint8_t* __restrict__ state;
+  uint8_t* __restrict__ miss;
+  uint32_t* __restrict__ fpop;       // frontier_r popcount: zeroed on crash
+  int32_t* __restrict__ cand;
+  int32_t* __restrict__ deg_live;
+  const int64_t* __restrict__ row_ptr;
+  const int32_t* __restrict__ col;
+  const int64_t* __restrict__ out_row_ptr;   // directed only
+  const int32_t* __restrict__ out_col;
+  gp_report* __restrict__ reports;
+  u64* __restrict__ stats;           // direct counters (cursor, cand)
+  u64* __restrict__ partial;
+  int64_t n, vbegin, vend;
+  int64_t report_cap;
+  u64 crash_key;
+  u64 p_thresh;                      // crash iff draw < p_thresh
+  int32_t p_always;                  // p_fail >= 1
+  int32_t miss_thr;
+  int32_t r;
+};
+
+__global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
+  WaveStats st;
+  ws_zero(st);
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t v = (int64_t)blockIdx.x * BLOCK + threadIdx.x; v < a.n; v += stride) {
+    uint8_t s = a.state[v];
+    if (!(s & ST_DOWN)) {
+      bool crash = (s & ST_PENDING) != 0;
+      if (!crash && (a.p_always || a.p_thresh))
+        crash = a.p_always || draw(a.crash_key, (u64)v) < a.p_thresh;
+      if (crash) {
+        s = (uint8_t)((s | ST_CRASHED) & ~ST_PENDING);
+        a.fpop[v] = 0;   // crash-stop: its frontier is never sent
+        if (v >= a.vbegin && v < a.vend) st.c[S_CRASHED] += 1;
+      }
+    }
+    if (s & ST_CRASHED) {
+      uint32_t mi = a.miss[v];
+      if (mi < 255) ++mi;
+      a.miss[v] = (uint8_t)mi;
+      if ((int)mi == a.miss_thr && !(s & ST_REMOVED)) {
+        const u64 slot = atomicAdd(&a.stats[S_CAND], 1ull);
+        a.cand[slot] = (int32_t)v;
+      }
+    }
+    a.state[v] = s;
+  }
+  // crashed counts: wave-reduce then flush (lanes hold different values here)
+  u64 c = st.c[S_CRASHED];
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) c += __shfl_xor(c, s);
+  st.c[S_CRASHED] = c;
+  flush_stats(st, a.partial);
+}
+
+// one wave per detection candidate: count live reporters (one per heartbeat
+// link), remove the vertex if anybody reports it, emit the reports.
+__global__ __launch_bounds__(BLOCK) void k_detect(LiveArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  WaveStats st;
+  ws_zero(st);
+  const int64_t ncand = (int64_t)a.stats[S_CAND];
+  const int64_t stride = (int64_t)gridDim.x * WAVES;
+  for (int64_t k = (int64_t)blockIdx.x * WAVES + wib; k < ncand; k += stride) {
+    const int v = a.cand[k];
+    uint32_t live = 0;
+    const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
+    for (int64_t j = b + lane; j < e; j += 64) live += !(a.state[a.col[j]] & ST_DOWN);
+    int64_t ob = 0, oe = 0;
+    if (a.out_row_ptr) {
+      ob = a.out_row_ptr[v];
+      oe = a.out_row_ptr[v + 1];
+      for (int64_t j = ob + lane; j < oe; j += 64) live += !(a.state[a.out_col[j]] & ST_DOWN);
+    }
+    const uint32_t tot = wave_sum_u32(live);
+    if (tot == 0) continue;   // nobody holds a link to it: never reported
+    if (lane == 0) a.state[v] |= ST_REMOVED;
+    for (int64_t j = b + lane; j < e; j += 64) atomicSub(&a.deg_live[a.col[j]], 1);
+    if (v >= a.vbegin && v < a.vend) {
+      st.c[S_REPORTS] += tot;
+      st.c[S_REMOVALS] += 1;
+      st.c[S_DUP] += tot - 1;
+      for (int pass = 0; pass < 2; ++pass) {
+        const int32_t* cl = pass == 0 ? a.col : a.out_col;
+        const int64_t pb = pass == 0 ? b : ob, pe = pass == 0 ? e : oe;
+        for (int64_t j0 = pb; j0 < pe; j0 += 64) {
+          const int64_t j = j0 + lane;
+          int u = -1;
+          bool rep = false;
+          if (j < pe) {
+            u = cl[j];
+            rep = !(a.state[u] & ST_DOWN);
+          }
+          const u64 m = __ballot(rep);
+          if (!m) continue;
+          u64 base = 0;
+          if (lane == 0) base = atomicAdd(&a.stats[S_REPORT_CURSOR], (u64)__popcll(m));
+          base = __shfl(base, 0);
+          if (rep) {
+            const u64 slot = base + (u64)lane_rank(m);
+            if ((int64_t)slot < a.report_cap) a.reports[slot] = gp_report{v, u, a.r};
+          }
+        }
+      }
+    }
+  }
+  flush_stats(st, a.partial);
+}
+
+// ---------------------------------------------------------------------------
+// per-message bit sums: cnt[m] += bit_m(row(v)), wsum[m] += weight(v)*bit_m(row(v))
+// over rows [0, count).  Lane l holds word l % W of vertex slot l / W; each lane
+// keeps 64 register counters per output.
+struct BitsumArgs {
+  const u64* __restrict__ rows;       // [count][W]
+  const uint32_t* __restrict__ guard; // optional: row valid iff guard[i] != 0
+  const int32_t* __restrict__ weight; // [count]
+  u64* __restrict__ cnt;              // [W*64] or null
+  u64* __restrict__ wsum;             // [W*64] or null
+  int64_t count;
+};
+
+template <int W, bool CNT, bool SUM>
+__global__ __launch_bounds__(BLOCK) void k_bitsum(BitsumArgs a) {
+  static_assert(W <= 64, "W <= 64");
+  constexpr int VPS = 64 / W;   // vertices per wave step
+  __shared__ uint32_t lc[CNT ? W * 64 : 1];
+  __shared__ uint32_t lsum[SUM ? W * 64 : 1];
+  for (int t = threadIdx.x; t < W * 64; t += BLOCK) {
+    if (CNT) lc[t] = 0;
+    if (SUM) lsum[t] = 0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int w = lane % W, q = lane / W;
+  uint32_t c[64], s[64];
+#pragma unroll
+  for (int b = 0; b < 64; ++b) {
+    c[b] = 0;
+    s[b] = 0;
+  }
+  const int64_t step = (int64_t)gridDim.x * WAVES * VPS;
+  for (int64_t i = ((int64_t)blockIdx.x * WAVES + wib) * VPS + q; i < a.count; i += step) {
+    u64 x = a.rows[i * W + w];
+    if (a.guard && a.guard[i] == 0) x = 0;
+    const uint32_t wt = SUM ? (uint32_t)max(a.weight[i], 0) : 0u;
+#pragma unroll
+    for (int b = 0; b < 64; ++b) {
+      const uint32_t bit = (uint32_t)(x >> b) & 1u;
+      if (CNT) c[b] += bit;
+      if (SUM) s[b] += bit * wt;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 64; ++b) {
+#pragma unroll
+    for (int st = W; st < 64; st <<= 1) {
+      if (CNT) c[b] += __shfl_xor(c[b], st);
+      if (SUM) s[b] += __shfl_xor(s[b], st);
+    }
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int b = 0; b < 64; ++b) {
+      if (CNT && c[b]) atomicAdd(&lc[w * 64 + b], c[b]);
+      if (SUM && s[b]) atomicAdd(&lsum[w * 64 + b], s[b]);
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < W * 64; t += BLOCK) {
+    if (CNT && lc[t]) atomicAdd(&a.cnt[t], (u64)lc[t]);
+    if (SUM && lsum[t]) atomicAdd(&a.wsum[t], (u64)lsum[t]);
+  }
+}
+
+__global__ void k_degree(const int64_t* __restrict__ rp, int32_t* __restrict__ deg, int64_t n) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n) deg[v] = (int32_t)(rp[v + 1] - rp[v]);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+
+static int grid_for(int64_t work, int64_t per_block) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > (int64_t)0x7fffffff) g = 0x7fffffff;
+  return (int)g;
+}
+
+static void fill_expand(Ctx* c, ExpandArgs& a) {
+  a.row_ptr = c->d_row_ptr;
+  a.col = c->d_col;
+  a.front = c->d_front[c->cur];
+  a.fpop = c->d_fpop[c->cur];
+  a.next = c->d_front[c->cur ^ 1];
+  a.fpop_next = c->d_fpop[c->cur ^ 1];
+  a.seen = c->d_seen;
+  a.seenpop = c->d_seenpop;
+  a.first = c->cfg.track_first ? c->d_first : nullptr;
+  a.digest = c->cfg.track_digest ? c->d_digest : nullptr;
+  a.state = c->d_state;
+  a.deg_live = c->d_deg_live;
+  a.partial = c->d_stats + 64;   // partial slots live behind the stats block
+  a.hub_items = c->d_hub_items;
+  a.hubs = c->d_hubs;
+  a.hub_item_ptr = c->d_hub_item_ptr;
+  a.hub_partial = c->d_hub_partial;
+  a.hub_pnz = c->d_hub_pnz;
+  a.vbegin = c->vbegin;
+  a.nloc = c->nloc();
+  a.m_total = c->m;
+  a.rr = c->round + 1;
+  a.hub_thr = c->cfg.hub_threshold;
+  a.vpw = 4;
+}
+
+template <int W>
+static void launch_expand_w(Ctx* c, ExpandArgs a) {
+  const int64_t per_block = (int64_t)WAVES * a.vpw;
+  if (a.nloc > 0)
+    hipLaunchKernelGGL(k_expand<W>, dim3(grid_for(a.nloc, per_block)), dim3(BLOCK), 0, c->stream, a);
+  if (c->n_hub_items > 0) {
+    ExpandArgs h = a;
+    h.n_items = c->n_hub_items;
+    hipLaunchKernelGGL(k_hub_partial<W>, dim3(grid_for(h.n_items, WAVES)), dim3(BLOCK), 0, c->stream, h);
+    h.n_items = c->n_hubs;
+    hipLaunchKernelGGL(k_hub_final<W>, dim3(grid_for(h.n_items, WAVES)), dim3(BLOCK), 0, c->stream, h);
+  }
+}
+
+static int launch_expand(Ctx* c) {
+  ExpandArgs a{};
+  fill_expand(c, a);
+  switch (c->words) {
+    case 1: launch_expand_w<1>(c, a); break;
+    case 2: launch_expand_w<2>(c, a); break;
+    case 4: launch_expand_w<4>(c, a); break;
+    case 8: launch_expand_w<8>(c, a); break;
+    case 16: launch_expand_w<16>(c, a); break;
+    case 32: launch_expand_w<32>(c, a); break;
+    case 64: launch_expand_w<64>(c, a); break;
+    default: return set_error(GP_EINVAL, "unsupported word count");
+  }
+  GP_HIP(hipGetLastError());
+  return 0;
+}
+
+template <int W>
+static void launch_bitsum_w(Ctx* c, BitsumArgs a, bool cnt, bool sum) {
+  const int grid = std::max(1, std::min(grid_for(a.count, (int64_t)WAVES * (64 / W)), c->cu_count * 2));
+  if (cnt && sum)
+    hipLaunchKernelGGL((k_bitsum<W, true, true>), dim3(grid), dim3(BLOCK), 0, c->stream, a);
+  else if (cnt)
+    hipLaunchKernelGGL((k_bitsum<W, true, false>), dim3(grid), dim3(BLOCK), 0, c->stream, a);
+  else if (sum)
+    hipLaunchKernelGGL((k_bitsum<W, false, true>), dim3(grid), dim3(BLOCK), 0, c->stream, a);
+}
+
+static int launch_bitsum(Ctx* c, BitsumArgs a, bool cnt, bool sum) {
+  if (a.count <= 0) return 0;
+  switch (c->words) {
+    case 1: launch_bitsum_w<1>(c, a, cnt, sum); break;
+    case 2: launch_bitsum_w<2>(c, a, cnt, sum); break;
+    case 4: launch_bitsum_w<4>(c, a, cnt, sum); break;
+    case 8: launch_bitsum_w<8>(c, a, cnt, sum); break;
+    case 16: launch_bitsum_w<16>(c, a, cnt, sum); break;
+    case 32: launch_bitsum_w<32>(c, a, cnt, sum); break;
+    case 64: launch_bitsum_w<64>(c, a, cnt, sum); break;
+    default: return set_error(GP_EINVAL, "unsupported word count");
+  }
+  GP_HIP(hipGetLastError());
+  return 0;
+}
+
+static int build_hubs(Ctx* c) {
+  c->h_hub_items.clear();
+  std::vector<int32_t> hubs, ptr;
+  const int64_t thr = c->cfg.hub_threshold;
+  if (!c->h_row_ptr.empty()) {
+    for (int64_t v = c->vbegin; v < c->vend; ++v) {
+      const int64_t b = c->h_row_ptr[v], e = c->h_row_ptr[v + 1];
+      if (e - b <= thr) continue;
+      ptr.push_back((int32_t)c->h_hub_items.size());
+      for (int64_t j = b; j < e; j += thr)
+        c->h_hub_items.push_back(HubItem{(int32_t)v, (int32_t)hubs.size(), j, std::min(e, j + thr)});
+      hubs.push_back((int32_t)v);
+    }
+  }
+  ptr.push_back((int32_t)c->h_hub_items.size());
+  c->n_hubs = (int64_t)hubs.size();
+  c->n_hub_items = (int64_t)c->h_hub_items.size();
+  GP_TRY(dalloc(&c->d_hub_items, c->h_hub_items.size()));
+  GP_TRY(dalloc(&c->d_hubs, hubs.size()));
+  GP_TRY(dalloc(&c->d_hub_item_ptr, ptr.size()));
+  GP_TRY(dalloc(&c->d_hub_pnz, c->h_hub_items.size()));
+  if (!c->h_hub_items.empty())
+    GP_HIP(hipMemcpy(c->d_hub_items, c->h_hub_items.data(), c->h_hub_items.size() * sizeof(HubItem),
+                     hipMemcpyHostToDevice));
+  if (!hubs.empty())
+    GP_HIP(hipMemcpy(c->d_hubs, hubs.data(), hubs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  GP_HIP(hipMemcpy(c->d_hub_item_ptr, ptr.data(), ptr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (c->words > 0) GP_TRY(dalloc(&c->d_hub_partial, c->h_hub_items.size() * (size_t)c->words));
+  return 0;
+}
+
+static int set_partition(Ctx* c, int32_t rank, int32_t nranks) {
+  if (nranks < 1 || rank < 0 || rank >= nranks) return set_error(GP_EINVAL, "bad rank/nranks");
+  c->rank = rank;
+  c->nranks = nranks;
+  c->slice = (c->n + nranks - 1) / nranks;
+  c->vbegin = std::min(c->n, (int64_t)rank * c->slice);
+  c->vend = std::min(c->n, c->vbegin + c->slice);
+  c->n_alloc = c->slice * nranks;
+  return build_hubs(c);
+}
+
+static void free_state(Ctx* c) {
+  for (int k = 0; k < 2; ++k) {
+    dfree(&c->d_front[k]);
+    dfree(&c->d_fpop[k]);
+  }
+  dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
+  dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports);
+  c->d_msg_fwd = nullptr;
+  dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
+  c->inject.clear();
+}
+
+int finish_graph(Ctx* c) {
+  free_state(c);
+  GP_TRY(dalloc(&c->d_deg_out, (size_t)c->n));
+  const int64_t* rp = c->directed ? c->d_out_row_ptr : c->d_row_ptr;
+  hipLaunchKernelGGL(k_degree, dim3(grid_for(c->n, 256)), dim3(256), 0, c->stream, rp, c->d_deg_out, c->n);
+  GP_HIP(hipGetLastError());
+  c->h_row_ptr.resize((size_t)c->n + 1);
+  GP_HIP(hipMemcpyAsync(c->h_row_ptr.data(), c->d_row_ptr, ((size_t)c->n + 1) * sizeof(int64_t),
+                        hipMemcpyDeviceToHost, c->stream));
+  GP_HIP(hipStreamSynchronize(c->stream));
+  c->m = 0;
+  c->words = 0;
+  return set_partition(c, c->rank, c->nranks);
+}
+
+// (re)allocate per-run state for the current graph/messages/config
+static int alloc_state(Ctx* c) {
+  if (c->n <= 0) return set_error(GP_ESTATE, "no graph loaded");
+  if (c->words <= 0) return set_error(GP_ESTATE, "no messages set");
+  const size_t W = (size_t)c->words, na = (size_t)c->n_alloc, nl = (size_t)std::max<int64_t>(c->nloc(), 1);
+  for (int k = 0; k < 2; ++k) {
+    GP_TRY(dalloc(&c->d_front[k], na * W));
+    GP_TRY(dalloc(&c->d_fpop[k], na));
+  }
+  GP_TRY(dalloc(&c->d_seen, nl * W));
+  GP_TRY(dalloc(&c->d_seenpop, nl));
+  if (c->cfg.track_first) GP_TRY(dalloc(&c->d_first, nl * W * 64));
+  else dfree(&c->d_first);
+  GP_TRY(dalloc(&c->d_digest, nl));
+  GP_TRY(dalloc(&c->d_state, na));
+  GP_TRY(dalloc(&c->d_miss, na));
+  GP_TRY(dalloc(&c->d_deg_live, na));
+  GP_TRY(dalloc(&c->d_cand, na));
+  GP_TRY(dalloc(&c->d_msg_cov, W * 64 * 4));   // [local cov | local fwd | global cov | global fwd]
+  c->d_msg_fwd = c->d_msg_cov + W * 64;
+  c->report_cap = std::max<int64_t>(c->cfg.report_capacity, 1);
+  GP_TRY(dalloc(&c->d_reports, (size_t)c->report_cap));
+  GP_TRY(dalloc(&c->d_hub_partial, std::max<size_t>(c->h_hub_items.size(), 1) * W));
+  return 0;
+}
+
+static bool state_ready(const Ctx* c) { return c->d_seen != nullptr && c->d_front[0] != nullptr; }
+
+}  // namespace gp
+
+using namespace gp;
+
+// ===========================================================================
+// C-ABI
+extern "C" {
+
+struct gp_ctx : public gp::Ctx {};
+
+int gp_abi_version(void) { return GP_ABI_VERSION; }
+const char* gp_last_error(void) { return g_err.c_str(); }
+
+int gp_device_count(int* n_out) {
+  if (!n_out) return set_error(GP_EINVAL, "null n_out");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *n_out = n;
+  return 0;
+}
+
+void gp_default_config(gp_config* cfg) {
+  if (!cfg) return;
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->track_first = 0;
+  cfg->track_digest = 1;
+  cfg->track_msg_forwards = 0;
+  cfg->churn = 0;
+  cfg->p_fail = 0.0;
+  cfg->churn_seed = 0;
+  cfg->miss_threshold = 3;     // 2 missed heartbeats + 1 unanswered PING (Peer.py:299-311)
+  cfg->hub_threshold = 4096;
+  cfg->report_capacity = 1 << 20;
+}
+
+int gp_create(int device, gp_ctx** out) {
+  if (!out) return set_error(GP_EINVAL, "null out");
+  *out = nullptr;
+  int ndev = 0;
+  GP_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return set_error(GP_EINVAL, "device index out of range");
+  GP_HIP(hipSetDevice(device));
+  gp_ctx* c = new gp_ctx();
+  c->device = device;
+  gp_default_config(&c->cfg);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->cu_count = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return set_error(GP_EHIP, "hipStreamCreate failed");
+  }
+  for (auto& e : c->ev) (void)hipEventCreate(&e);
+  if (dalloc(&c->d_stats, 64 + (size_t)NPART * NST) != 0) {
+    gp_destroy(c);
+    return GP_ENOMEM;
+  }
+  (void)hipMemset(c->d_stats, 0, (64 + (size_t)NPART * NST) * sizeof(u64));
+  (void)hipHostMalloc((void**)&c->h_stats, 64 * sizeof(u64), hipHostMallocDefault);
+  *out = c;
+  return 0;
+}
+
+void gp_destroy(gp_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
+  dfree(&c->d_deg_out); dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
+  for (int k = 0; k < 2; ++k) { dfree(&c->d_front[k]); dfree(&c->d_fpop[k]); }
+  dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
+  dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_stats);
+  dfree(&c->d_hub_items); dfree(&c->d_hubs); dfree(&c->d_hub_item_ptr);
+  dfree(&c->d_hub_partial); dfree(&c->d_hub_pnz);
+  if (c->h_stats) (void)hipHostFree(c->h_stats);
+  for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int gp_configure(gp_ctx* c, const gp_config* cfg) {
+  if (!c || !cfg) return set_error(GP_EINVAL, "null argument");
+  if (cfg->p_fail < 0.0 || !(cfg->p_fail <= 1.0)) return set_error(GP_EINVAL, "p_fail must be in [0,1]");
+  if (cfg->miss_threshold < 1 || cfg->miss_threshold > 254) return set_error(GP_EINVAL, "miss_threshold in [1,254]");
+  if (cfg->hub_threshold < 64) return set_error(GP_EINVAL, "hub_threshold must be >= 64");
+  if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
+  GP_HIP(hipSetDevice(c->device));
+  const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
+  c->cfg = *cfg;
+  if (c->n > 0 && hub_changed) GP_TRY(build_hubs(c));
+  if (state_ready(c)) GP_TRY(alloc_state(c));
+  return 0;
+}
+
+int gp_load_graph(gp_ctx* c, int64_t n, int64_t nnz, const int64_t* row_ptr, const int32_t* col,
+                  int32_t directed, const int64_t* out_row_ptr, const int32_t* out_col) {
+  if (!c || !row_ptr || (nnz > 0 && !col)) return set_error(GP_EINVAL, "null argument");
+  if (n <= 0 || n >= (int64_t)0x7fffffff) return set_error(GP_EINVAL, "n out of range");
+  if (nnz < 0 || row_ptr[0] != 0 || row_ptr[n] != nnz) return set_error(GP_EINVAL, "row_ptr inconsistent with nnz");
+  for (int64_t v = 0; v < n; ++v)
+    if (row_ptr[v + 1] < row_ptr[v]) return set_error(GP_EINVAL, "row_ptr not monotone");
+  for (int64_t j = 0; j < nnz; ++j)
+    if (col[j] < 0 || col[j] >= n) return set_error(GP_EINVAL, "col index out of range");
+  GP_HIP(hipSetDevice(c->device));
+  std::vector<int64_t> orp;
+  std::vector<int32_t> ocol;
+  if (directed) {
+    if (out_row_ptr && out_col) {
+      if (out_row_ptr[0] != 0 || out_row_ptr[n] != nnz) return set_error(GP_EINVAL, "out CSR inconsistent");
+      orp.assign(out_row_ptr, out_row_ptr + n + 1);
+      ocol.assign(out_col, out_col + nnz);
+    } else {   // transpose the in-CSR: out(u) = {v : u in In(v)}
+      orp.assign((size_t)n + 1, 0);
+      for (int64_t j = 0; j < nnz; ++j) orp[(size_t)col[j] + 1]++;
+      for (int64_t v = 0; v < n; ++v) orp[v + 1] += orp[v];
+      ocol.resize((size_t)nnz);
+      std::vector<int64_t> cur(orp.begin(), orp.end() - 1);
+      for (int64_t v = 0; v < n; ++v)
+        for (int64_t j = row_ptr[v]; j < row_ptr[v + 1]; ++j) ocol[cur[col[j]]++] = (int32_t)v;
+    }
+  }
+  c->n = n;
+  c->nnz = nnz;
+  c->directed = directed ? 1 : 0;
+  GP_TRY(dalloc(&c->d_row_ptr, (size_t)n + 1));
+  GP_TRY(dalloc(&c->d_col, (size_t)nnz));
+  GP_HIP(hipMemcpy(c->d_row_ptr, row_ptr, ((size_t)n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (nnz) GP_HIP(hipMemcpy(c->d_col, col, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (directed) {
+    GP_TRY(dalloc(&c->d_out_row_ptr, (size_t)n + 1));
+    GP_TRY(dalloc(&c->d_out_col, (size_t)nnz));
+    GP_HIP(hipMemcpy(c->d_out_row_ptr, orp.data(), ((size_t)n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    if (nnz) GP_HIP(hipMemcpy(c->d_out_col, ocol.data(), (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+  } else {
+    dfree(&c->d_out_row_ptr);
+    dfree(&c->d_out_col);
+  }
+  return finish_graph(c);
+}
+
+int gp_build_chung_lu(gp_ctx* c, int64_t n, double dbar, double gamma, uint64_t seed) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (n < 2 || n >= (int64_t)0x7fffffff) return set_error(GP_EINVAL, "n out of range");
+  if (!(dbar > 0.0) || !(gamma > 2.0)) return set_error(GP_EINVAL, "need dbar > 0 and gamma > 2");
+  GP_HIP(hipSetDevice(c->device));
+  GP_TRY(build_chung_lu(c, n, dbar, gamma, seed));
+  return finish_graph(c);
+}
+
+int gp_set_partition(gp_ctx* c, int32_t rank, int32_t nranks) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (c->n <= 0) return set_error(GP_ESTATE, "load a graph first");
+  GP_HIP(hipSetDevice(c->device));
+  GP_TRY(set_partition(c, rank, nranks));
+  if (state_ready(c)) GP_TRY(alloc_state(c));
+  return 0;
+}
+
+int gp_get_partition(gp_ctx* c, int64_t* vbegin, int64_t* vend) {
+  if (!c || !vbegin || !vend) return set_error(GP_EINVAL, "null argument");
+  *vbegin = c->vbegin;
+  *vend = c->vend;
+  return 0;
+}
+
+int gp_comm_unique_id(void* out128) {
+  if (!out128) return set_error(GP_EINVAL, "null out");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  GP_RCCL(ncclGetUniqueId(&id));
+  std::memcpy(out128, &id, sizeof(id));
+  return 0;
+}
+
+int gp_comm_init(gp_ctx* c, const void* uid, int32_t nranks, int32_t rank) {
+  if (!c || !uid) return set_error(GP_EINVAL, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return set_error(GP_EINVAL, "bad rank/nranks");
+  GP_HIP(hipSetDevice(c->device));
+  if (c->comm) {
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  if (nranks == 1) return 0;
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  GP_RCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
+  return 0;
+}
+
+int gp_set_messages(gp_ctx* c, int32_t m, const int32_t* origin, const int32_t* inject_round) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (c->n <= 0) return set_error(GP_ESTATE, "load a graph first");
+  if (m < 1 || m > 4096) return set_error(GP_EINVAL, "m must be in [1, 4096] per context");
+  if (!origin) return set_error(GP_EINVAL, "null origin");
+  GP_HIP(hipSetDevice(c->device));
+  int words = 1;
+  while (words * 64 < m) words <<= 1;
+  // group by (round, origin)
+  std::vector<std::pair<std::pair<int32_t, int32_t>, int32_t>> key((size_t)m);
+  int32_t last = -1;
+  for (int32_t k = 0; k < m; ++k) {
+    const int32_t o = origin[k];
+    const int32_t r = inject_round ? inject_round[k] : 0;
+    if (o < 0 || o >= c->n) return set_error(GP_EINVAL, "origin out of range");
+    if (r < 0 || r > 253) return set_error(GP_EINVAL, "inject_round must be in [0, 253]");
+    key[(size_t)k] = {{r, o}, k};
+    last = std::max(last, r);
+  }
+  std::sort(key.begin(), key.end());
+  std::vector<int32_t> g_origin;
+  std::vector<u64> g_bits;
+  std::vector<uint32_t> g_cnt;
+  c->inject.clear();
+  for (size_t k = 0; k < key.size();) {
+    const int32_t r = key[k].first.first, o = key[k].first.second;
+    auto& span = c->inject[r];
+    if (span.cnt == 0) span.off = (int64_t)g_origin.size();
+    g_origin.push_back(o);
+    g_bits.resize(g_bits.size() + (size_t)words, 0);
+    u64* row = g_bits.data() + g_bits.size() - words;
+    uint32_t cnt = 0;
+    while (k < key.size() && key[k].first.first == r && key[k].first.second == o) {
+      const int32_t msg = key[k].second;
+      row[msg >> 6] |= 1ull << (msg & 63);
+      ++cnt;
+      ++k;
+    }
+    g_cnt.push_back(cnt);
+    span.cnt++;
+  }
+  c->m = m;
+  c->last_inject_round = last;
+  const bool realloc = words != c->words;
+  c->words = words;
+  GP_TRY(dalloc(&c->d_inj_origin, g_origin.size()));
+  GP_TRY(dalloc(&c->d_inj_bits, g_bits.size()));
+  GP_TRY(dalloc(&c->d_inj_cnt, g_cnt.size()));
+  GP_HIP(hipMemcpy(c->d_inj_origin, g_origin.data(), g_origin.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  GP_HIP(hipMemcpy(c->d_inj_bits, g_bits.data(), g_bits.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+  GP_HIP(hipMemcpy(c->d_inj_cnt, g_cnt.data(), g_cnt.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  if (realloc || !state_ready(c)) GP_TRY(alloc_state(c));
+  return 0;
+}
+
+int gp_reset(gp_ctx* c) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (!state_ready(c)) GP_TRY(alloc_state(c));
+  GP_HIP(hipSetDevice(c->device));
+  const size_t W = (size_t)c->words, na = (size_t)c->n_alloc, nl = (size_t)std::max<int64_t>(c->nloc(), 1);
+  hipStream_t s = c->stream;
+  GP_HIP(hipMemsetAsync(c->d_seen, 0, nl * W * 8, s));
+  GP_HIP(hipMemsetAsync(c->d_seenpop, 0, nl * 4, s));
+  GP_HIP(hipMemsetAsync(c->d_fpop[0], 0, na * 4, s));
+  GP_HIP(hipMemsetAsync(c->d_fpop[1], 0, na * 4, s));
+  if (c->d_first) GP_HIP(hipMemsetAsync(c->d_first, 0xFF, nl * W * 64, s));
+  GP_HIP(hipMemsetAsync(c->d_digest, 0, nl * 8, s));
+  GP_HIP(hipMemsetAsync(c->d_state, 0, na, s));
+  GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
+  GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
+  GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToDevice, s));
+  GP_HIP(hipMemsetAsync(c->d_msg_cov, 0, W * 64 * 4 * 8, s));
+  GP_HIP(hipMemsetAsync(c->d_stats, 0, (64 + (size_t)NPART * NST) * 8, s));
+  c->cur = 0;
+  c->round = 0;
+  c->liveness_active = c->cfg.churn != 0;
+  c->pending_crash = false;
+  c->msg_forwards_valid = true;
+  c->last_reports = 0;
+  GP_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+int gp_crash(gp_ctx* c, int32_t nverts, const int32_t* verts) {
+  if (!c || (nverts > 0 && !verts)) return set_error(GP_EINVAL, "null argument");
+  if (!state_ready(c)) return set_error(GP_ESTATE, "gp_reset first");
+  GP_HIP(hipSetDevice(c->device));
+  std::vector<uint8_t> st((size_t)c->n);
+  GP_HIP(hipMemcpy(st.data(), c->d_state, (size_t)c->n, hipMemcpyDeviceToHost));
+  for (int32_t k = 0; k < nverts; ++k) {
+    if (verts[k] < 0 || verts[k] >= c->n) return set_error(GP_EINVAL, "vertex out of range");
+    if (!(st[verts[k]] & ST_DOWN)) st[verts[k]] |= ST_PENDING;
+  }
+  GP_HIP(hipMemcpy(c->d_state, st.data(), (size_t)c->n, hipMemcpyHostToDevice));
+  if (nverts > 0) {
+    c->liveness_active = true;
+    c->pending_crash = true;
+  }
+  return 0;
+}
+
+}  // extern "C"
+
+namespace gp {
+
+// phases L_r, I_r, E_r of one round on one context (no host sync)
+static int round_launch(Ctx* c) {
+  if (!state_ready(c) || c->words <= 0) return set_error(GP_ESTATE, "gp_set_messages + gp_reset first");
+  if (c->round > 253) return set_error(GP_ESTATE, "round limit (254) reached");
+  GP_HIP(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  u64* stats = c->d_stats;
+  u64* partial = c->d_stats + 64;
+  const int r = c->round;
+  GP_HIP(hipMemsetAsync(stats, 0, 64 * sizeof(u64), s));
+  GP_HIP(hipEventRecord(c->ev[0], s));
+  if (c->liveness_active) {
+    c->msg_forwards_valid = c->msg_forwards_valid && (c->cfg.track_msg_forwards != 0);
+    LiveArgs la{};
+    la.state = c->d_state;
+    la.miss = c->d_miss;
+    la.fpop = c->d_fpop[c->cur];
+    la.cand = c->d_cand;
+    la.deg_live = c->d_deg_live;
+    la.row_ptr = c->d_row_ptr;
+    la.col = c->d_col;
+    la.out_row_ptr = c->directed ? c->d_out_row_ptr : nullptr;
+    la.out_col = c->directed ? c->d_out_col : nullptr;
+    la.reports = c->d_reports;
+    la.stats = stats;
+    la.partial = partial;
+    la.n = c->n;
+    la.vbegin = c->vbegin;
+    la.vend = c->vend;
+    la.report_cap = c->report_cap;
+    la.crash_key = stream_key(c->cfg.churn_seed, STREAM_CRASH + (uint64_t)r);
+    const double p = c->cfg.churn ? c->cfg.p_fail : 0.0;
+    la.p_always = p >= 1.0;
+    la.p_thresh = (p > 0.0 && p < 1.0) ? (uint64_t)std::ldexp(p, 64) : 0ull;
+    la.miss_thr = c->cfg.miss_threshold;
+    la.r = r;
+    hipLaunchKernelGGL(k_churn, dim3(std::min(grid_for(c->n, BLOCK), c->cu_count * 8)), dim3(BLOCK), 0, s, la);
+    hipLaunchKernelGGL(k_detect, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, la);
+    GP_HIP(hipGetLastError());
+    c->pending_crash = false;
+  }
+
+  auto it = c->inject.find(r);
+  if (it != c->inject.end() && it->second.cnt > 0) {
+    InjectArgs ia{};
+    ia.origin = c->d_inj_origin;
+    ia.bits = c->d_inj_bits;
+    ia.cnt = c->d_inj_cnt;
+    ia.front = c->d_front[c->cur];
+    ia.fpop = c->d_fpop[c->cur];
+    ia.seen = c->d_seen;
+    ia.seenpop = c->d_seenpop;
+    ia.first = c->cfg.track_first ? c->d_first : nullptr;
+    ia.digest = c->cfg.track_digest ? c->d_digest : nullptr;
+    ia.state = c->d_state;
+    ia.partial = partial;
+    ia.off = it->second.off;
+    ia.groups = it->second.cnt;
+    ia.vbegin = c->vbegin;
+    ia.vend = c->vend;
+    ia.words = c->words;
+    ia.r = r;
+    hipLaunchKernelGGL(k_inject, dim3(grid_for(ia.groups, WAVES)), dim3(BLOCK), 0, s, ia);
+    GP_HIP(hipGetLastError());
+  }
+
+  if (c->cfg.track_msg_forwards) {   // sends of round r per message (owned senders)
+    BitsumArgs b{};
+    b.rows = c->d_front[c->cur] + (size_t)c->vbegin * c->words;
+    b.guard = c->d_fpop[c->cur] + c->vbegin;
+    b.weight = c->d_deg_live + c->vbegin;
+    b.cnt = nullptr;
+    b.wsum = c->d_msg_fwd;
+    b.count = c->nloc();
+    GP_TRY(launch_bitsum(c, b, false, true));
+  }
+
+  GP_HIP(hipEventRecord(c->ev[1], s));
+  GP_TRY(launch_expand(c));
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(BLOCK), 0, s, partial, stats);
+  GP_HIP(hipGetLastError());
+  GP_HIP(hipEventRecord(c->ev[2], s));
+
+  return 0;
+}
+
+// X_r over RCCL: all-gather the owned next rows + popcounts, sum the counters
+static int round_exchange_rccl(Ctx* c) {
+  if (!c->comm) return 0;
+  hipStream_t s = c->stream;
+  const int nx = c->cur ^ 1;
+  const size_t W = (size_t)c->words;
+  GP_RCCL(ncclGroupStart());
+  GP_RCCL(ncclAllGather(c->d_front[nx] + (size_t)c->rank * c->slice * W, c->d_front[nx],
+                        (size_t)c->slice * W, ncclUint64, c->comm, s));
+  GP_RCCL(ncclAllGather(c->d_fpop[nx] + (size_t)c->rank * c->slice, c->d_fpop[nx],
+                        (size_t)c->slice, ncclUint32, c->comm, s));
+  // the report cursor (slot S_REPORT_CURSOR) stays rank-local
+  GP_RCCL(ncclAllReduce(c->d_stats, c->d_stats, S_REPORT_CURSOR, ncclUint64, ncclSum, c->comm, s));
+  GP_RCCL(ncclGroupEnd());
+  return 0;
+}
+
+static int round_collect(Ctx* c, gp_round_stats* out) {
+  hipStream_t s = c->stream;
+  const int r = c->round;
+  GP_HIP(hipEventRecord(c->ev[3], s));
+  GP_HIP(hipMemcpyAsync(c->h_stats, c->d_stats, 64 * sizeof(u64), hipMemcpyDeviceToHost, s));
+  GP_HIP(hipStreamSynchronize(s));
+  const u64* h = c->h_stats;
+  if (out) {
+    std::memset(out, 0, sizeof(*out));
+    out->round = r;
+    out->injected = h[S_INJECTED];
+    out->lost = h[S_LOST];
+    out->new_bits = h[S_NEW_BITS];
+    out->receivers = h[S_RECEIVERS];
+    out->sends = h[S_SENDS];
+    out->active = h[S_ACTIVE];
+    out->crashed = h[S_CRASHED];
+    out->reports = h[S_REPORTS];
+    out->removals = h[S_REMOVALS];
+    out->dup_reports = h[S_DUP];
+    out->arcs_scanned = h[S_ARCS];
+    out->rows_gathered = h[S_GATHERED];
+    out->seen_rows_read = h[S_SEEN_READ];
+    out->rows_written = h[S_WRITTEN];
+    out->vertices_visited = h[S_VISITED];
+    out->overflow = (int64_t)h[S_REPORT_CURSOR] > c->report_cap ? 1 : 0;
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
+    out->expand_ms = ms;
+    (void)hipEventElapsedTime(&ms, c->ev[2], c->ev[3]);
+    out->exchange_ms = ms;
+    (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
+    out->round_ms = ms;
+  }
+  c->last_reports = (int64_t)h[S_REPORT_CURSOR];
+  c->cur ^= 1;
+  c->round = r + 1;
+  return 0;
+}
+
+}  // namespace gp
+
+extern "C" {
+
+int gp_round(gp_ctx* c, gp_round_stats* out) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  GP_TRY(round_launch(c));
+  GP_TRY(round_exchange_rccl(c));
+  return round_collect(c, out);
+}
+
+int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
+  if (!ctxs || nctx < 1) return set_error(GP_EINVAL, "bad context list");
+  for (int32_t k = 0; k < nctx; ++k) {
+    Ctx* c = ctxs[k];
+    if (!c) return set_error(GP_EINVAL, "null ctx in group");
+    if (c->comm) return set_error(GP_EINVAL, "group rounds exchange without RCCL");
+    if (c->nranks != nctx || c->rank != k) return set_error(GP_EINVAL, "ctxs[k] must own partition k of nctx");
+    if (c->round != ctxs[0]->round || c->n != ctxs[0]->n || c->words != ctxs[0]->words)
+      return set_error(GP_EINVAL, "contexts out of step");
+  }
+  for (int32_t k = 0; k < nctx; ++k) GP_TRY(round_launch(ctxs[k]));
+  for (int32_t k = 0; k < nctx; ++k) {
+    GP_HIP(hipSetDevice(ctxs[k]->device));
+    GP_HIP(hipStreamSynchronize(ctxs[k]->stream));
+  }
+  // X_r by device-to-device copies: every context receives every other's slice
+  for (int32_t d = 0; d < nctx; ++d) {
+    Ctx* dst = ctxs[d];
+    GP_HIP(hipSetDevice(dst->device));
+    const int nx = dst->cur ^ 1;
+    const size_t W = (size_t)dst->words;
+    for (int32_t k = 0; k < nctx; ++k) {
+      if (k == d) continue;
+      Ctx* src = ctxs[k];
+      const int64_t b = src->vbegin, e = src->vend;
+      if (e <= b) continue;
+      GP_HIP(hipMemcpyAsync(dst->d_front[nx] + (size_t)b * W, src->d_front[src->cur ^ 1] + (size_t)b * W,
+                            (size_t)(e - b) * W * 8, hipMemcpyDefault, dst->stream));
+      GP_HIP(hipMemcpyAsync(dst->d_fpop[nx] + b, src->d_fpop[src->cur ^ 1] + b, (size_t)(e - b) * 4,
+                            hipMemcpyDefault, dst->stream));
+    }
+  }
+  gp_round_stats sum;
+  std::memset(&sum, 0, sizeof(sum));
+  for (int32_t k = 0; k < nctx; ++k) {
+    gp_round_stats st;
+    GP_TRY(round_collect(ctxs[k], &st));
+    sum.round = st.round;
+    sum.overflow |= st.overflow;
+    sum.injected += st.injected; sum.lost += st.lost; sum.new_bits += st.new_bits;
+    sum.receivers += st.receivers; sum.sends += st.sends; sum.active += st.active;
+    sum.crashed += st.crashed; sum.reports += st.reports; sum.removals += st.removals;
+    sum.dup_reports += st.dup_reports; sum.arcs_scanned += st.arcs_scanned;
+    sum.rows_gathered += st.rows_gathered; sum.seen_rows_read += st.seen_rows_read;
+    sum.rows_written += st.rows_written; sum.vertices_visited += st.vertices_visited;
+    sum.expand_ms = std::max(sum.expand_ms, st.expand_ms);
+    sum.exchange_ms = std::max(sum.exchange_ms, st.exchange_ms);
+    sum.round_ms = std::max(sum.round_ms, st.round_ms);
+  }
+  if (out) *out = sum;
+  return 0;
+}
+
+int gp_run(gp_ctx* c, int32_t max_rounds, gp_round_stats* per_round, int32_t* rounds_out) {
+  if (!c || max_rounds < 1) return set_error(GP_EINVAL, "bad argument");
+  int32_t done = 0;
+  for (int32_t k = 0; k < max_rounds; ++k) {
+    gp_round_stats st;
+    GP_TRY(gp_round(c, &st));
+    if (per_round) per_round[k] = st;
+    ++done;
+    if (st.new_bits == 0 && st.round >= c->last_inject_round) break;
+  }
+  if (rounds_out) *rounds_out = done;
+  return 0;
+}
+
+int gp_finalize_messages(gp_ctx* c) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (!state_ready(c)) return set_error(GP_ESTATE, "no run state");
+  GP_HIP(hipSetDevice(c->device));
+  const size_t M = (size_t)c->words * 64;
+  hipStream_t s = c->stream;
+  u64* cov = c->d_msg_cov;
+  u64* fwd_local = c->d_msg_fwd;
+  u64* gcov = c->d_msg_cov + 2 * M;
+  u64* gfwd = c->d_msg_cov + 3 * M;
+  const bool fwd_from_seen = !c->liveness_active && !c->cfg.track_msg_forwards;
+  GP_HIP(hipMemsetAsync(cov, 0, M * 8, s));
+  if (fwd_from_seen) GP_HIP(hipMemsetAsync(fwd_local, 0, M * 8, s));
+  BitsumArgs b{};
+  b.rows = c->d_seen;
+  b.guard = nullptr;
+  b.weight = c->d_deg_out + c->vbegin;
+  b.cnt = cov;
+  b.wsum = fwd_from_seen ? fwd_local : nullptr;
+  b.count = c->nloc();
+  GP_TRY(launch_bitsum(c, b, true, fwd_from_seen));
+  if (c->comm) {
+    GP_RCCL(ncclGroupStart());
+    GP_RCCL(ncclAllReduce(cov, gcov, M, ncclUint64, ncclSum, c->comm, s));
+    GP_RCCL(ncclAllReduce(fwd_local, gfwd, M, ncclUint64, ncclSum, c->comm, s));
+    GP_RCCL(ncclGroupEnd());
+  } else {
+    GP_HIP(hipMemcpyAsync(gcov, cov, M * 8, hipMemcpyDeviceToDevice, s));
+    GP_HIP(hipMemcpyAsync(gfwd, fwd_local, M * 8, hipMemcpyDeviceToDevice, s));
+  }
+  GP_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
+  if (!c || !host) return set_error(GP_EINVAL, "null argument");
+  GP_HIP(hipSetDevice(c->device));
+  GP_HIP(hipStreamSynchronize(c->stream));
+  const int64_t W = c->words, nl = c->nloc(), M = c->m, n = c->n;
+  auto need = [&](int64_t b) -> int {
+    if (bytes != b) return set_error(GP_EINVAL, "bytes mismatch: expected " + std::to_string(b));
+    return 0;
+  };
+  const bool run = state_ready(c);
+  switch (what) {
+    case GP_SEEN:
+      if (!run) return set_error(GP_ESTATE, "no run state");
+      GP_TRY(need(nl * W * 8));
+      if (bytes) GP_HIP(hipMemcpy(host, c->d_seen, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case GP_FIRST:
+      if (!run) return set_error(GP_ESTATE, "no run state");
+      if (!c->d_first || !c->cfg.track_first) return set_error(GP_ENOTRACK, "track_first is off");
+      GP_TRY(need(nl * M));
+      if (bytes)
+        GP_HIP(hipMemcpy2D(host, (size_t)M, c->d_first, (size_t)W * 64, (size_t)M, (size_t)nl,
+                           hipMemcpyDeviceToHost));
+      return 0;
+    case GP_DIGEST:
+      if (!run) return set_error(GP_ESTATE, "no run state");
+      if (!c->cfg.track_digest) return set_error(GP_ENOTRACK, "track_digest is off");
+      GP_TRY(need(nl * 8));
+      if (bytes) GP_HIP(hipMemcpy(host, c->d_digest, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case GP_COVERAGE:
+    case GP_FORWARDS: {
+      if (!run) return set_error(GP_ESTATE, "no run state");
+      if (what == GP_FORWARDS && !c->msg_forwards_valid && c->liveness_active)
+        return set_error(GP_ENOTRACK, "churn run without track_msg_forwards");
+      GP_TRY(need(M * 8));
+      const size_t MM = (size_t)W * 64;
+      const u64* src = c->d_msg_cov + (what == GP_COVERAGE ? 2 * MM : 3 * MM);
+      GP_HIP(hipMemcpy(host, src, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    }
+    case GP_STATE:
+    case GP_MISS:
+      if (!run) return set_error(GP_ESTATE, "no run state");
+      GP_TRY(need(n));
+      GP_HIP(hipMemcpy(host, what == GP_STATE ? c->d_state : c->d_miss, (size_t)n, hipMemcpyDeviceToHost));
+      return 0;
+    case GP_DEG_LIVE:
+      if (!run) return set_error(GP_ESTATE, "no run state");
+      GP_TRY(need(n * 4));
+      GP_HIP(hipMemcpy(host, c->d_deg_live, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case GP_ROW_PTR:
+      if (n <= 0) return set_error(GP_ESTATE, "no graph");
+      GP_TRY(need((n + 1) * 8));
+      GP_HIP(hipMemcpy(host, c->d_row_ptr, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case GP_COL:
+      if (n <= 0) return set_error(GP_ESTATE, "no graph");
+      GP_TRY(need(c->nnz * 4));
+      if (bytes) GP_HIP(hipMemcpy(host, c->d_col, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case GP_FPOP:
+      if (!run) return set_error(GP_ESTATE, "no run state");
+      GP_TRY(need(n * 4));
+      GP_HIP(hipMemcpy(host, c->d_fpop[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case GP_FRONTIER: {
+      if (!run) return set_error(GP_ESTATE, "no run state");
+      GP_TRY(need(n * W * 8));
+      std::vector<uint32_t> fp((size_t)n);
+      GP_HIP(hipMemcpy(fp.data(), c->d_fpop[c->cur], (size_t)n * 4, hipMemcpyDeviceToHost));
+      GP_HIP(hipMemcpy(host, c->d_front[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
+      uint64_t* h = static_cast<uint64_t*>(host);
+      for (int64_t v = 0; v < n; ++v)
+        if (!fp[v]) std::memset(h + v * W, 0, (size_t)W * 8);
+      return 0;
+    }
+    default:
+      return set_error(GP_EINVAL, "unknown gp_what");
+  }
+}
+
+int gp_reports(gp_ctx* c, gp_report* buf, int64_t cap, int64_t* n_out) {
+  if (!c || !n_out || (cap > 0 && !buf)) return set_error(GP_EINVAL, "null argument");
+  GP_HIP(hipSetDevice(c->device));
+  const int64_t total = c->last_reports;
+  *n_out = total;
+  const int64_t k = std::min(std::min(total, cap), c->report_cap);
+  if (k > 0) GP_HIP(hipMemcpy(buf, c->d_reports, (size_t)k * sizeof(gp_report), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gp_synchronize(gp_ctx* c) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  GP_HIP(hipSetDevice(c->device));
+  GP_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int gp_info(gp_ctx* c, int64_t* n, int64_t* nnz, int32_t* m, int32_t* words) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (n) *n = c->n;
+  if (nnz) *nnz = c->nnz;
+  if (m) *m = c->m;
+  if (words) *words = c->words;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+// gp_internal.h -- context layout and helpers shared by the translation units of
+// libgossip_hip.so.  Not part of the ABI (include/gossip_capi.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/gossip_capi.h"
+#include "gp_common.h"
+
+namespace gp {
+
+typedef unsigned long long u64;
+
+// stats slots in the device counter block (u64 each)
+enum StatSlot {
+  S_INJECTED = 0, S_LOST, S_NEW_BITS, S_RECEIVERS, S_SENDS, S_ACTIVE, S_CRASHED,
+  S_REPORTS, S_REMOVALS, S_DUP, S_ARCS, S_GATHERED, S_SEEN_READ, S_WRITTEN,
+  S_VISITED, S_REPORT_CURSOR, S_CAND, NSTAT = 24
+};
+
+struct HubItem {       // one wave's share of a hub's in-list
+  int32_t v;           // hub vertex
+  int32_t hub;         // index into the hub table
+  int64_t beg, end;    // arc range
+};
+
+struct InjectSpan { int64_t off; int64_t cnt; };
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  gp_config cfg{};
+
+  // graph (full, replicated on every rank)
+  int64_t n = 0, nnz = 0;
+  int directed = 0;
+  int64_t* d_row_ptr = nullptr;
+  int32_t* d_col = nullptr;
+  int64_t* d_out_row_ptr = nullptr;   // directed only
+  int32_t* d_out_col = nullptr;
+  int32_t* d_deg_out = nullptr;
+  std::vector<int64_t> h_row_ptr;     // host copy (hub table, partition)
+
+  // partition
+  int32_t rank = 0, nranks = 1;
+  int64_t slice = 0;                  // rows per rank (padded)
+  int64_t vbegin = 0, vend = 0;       // owned vertices
+  int64_t n_alloc = 0;                // nranks * slice
+
+  // messages
+  int32_t m = 0, words = 0;
+  std::map<int32_t, InjectSpan> inject;   // round -> groups
+  int32_t last_inject_round = -1;
+  int32_t* d_inj_origin = nullptr;
+  u64* d_inj_bits = nullptr;
+  uint32_t* d_inj_cnt = nullptr;
+
+  // per-run state
+  u64* d_front[2] = {nullptr, nullptr};   // [n_alloc][W]
+  uint32_t* d_fpop[2] = {nullptr, nullptr};    // [n_alloc]
+  int cur = 0;
+  u64* d_seen = nullptr;       // [nloc][W]
+  uint32_t* d_seenpop = nullptr;    // [nloc]
+  uint8_t* d_first = nullptr;       // [nloc][W*64]
+  u64* d_digest = nullptr;     // [nloc]
+  uint8_t* d_state = nullptr;       // [n_alloc]
+  uint8_t* d_miss = nullptr;        // [n_alloc]
+  int32_t* d_deg_live = nullptr;    // [n_alloc]
+  int32_t* d_cand = nullptr;        // [n] detection candidates of a round
+  u64* d_msg_cov = nullptr;    // [W*64]
+  u64* d_msg_fwd = nullptr;    // [W*64]
+  gp_report* d_reports = nullptr;
+  int64_t report_cap = 0;
+  u64* d_stats = nullptr;      // [NSTAT]
+  u64* h_stats = nullptr;      // pinned [NSTAT]
+  int32_t round = 0;
+  bool liveness_active = false;
+  bool pending_crash = false;
+  bool msg_forwards_valid = true;
+  int64_t last_reports = 0;
+
+  // hub split
+  std::vector<HubItem> h_hub_items;
+  HubItem* d_hub_items = nullptr;
+  int32_t* d_hubs = nullptr;          // hub vertex per hub
+  int32_t* d_hub_item_ptr = nullptr;  // [n_hubs+1]
+  u64* d_hub_partial = nullptr;  // [items][W]
+  uint32_t* d_hub_pnz = nullptr;      // [items]
+  int64_t n_hubs = 0, n_hub_items = 0;
+
+  // rccl
+  ncclComm_t comm = nullptr;
+
+  // kernel geometry
+  int cu_count = 256;
+
+  int64_t nloc() const { return vend - vbegin; }
+};
+
+// error helpers (thread-local message, negative status)
+int set_error(int code, const std::string& msg);
+#define GP_HIP(call)                                                              \
+  do {                                                                            \
+    hipError_t _e = (call);                                                       \
+    if (_e != hipSuccess)                                                         \
+      return ::gp::set_error(GP_EHIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+#define GP_RCCL(call)                                                             \
+  do {                                                                            \
+    ncclResult_t _r = (call);                                                     \
+    if (_r != ncclSuccess)                                                        \
+      return ::gp::set_error(GP_ERCCL, std::string(#call) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+#define GP_TRY(expr)                                                              \
+  do { int _rc = (expr); if (_rc != 0) return _rc; } while (0)
+
+template <class T>
+int dalloc(T** p, size_t count) {
+  if (*p) { (void)hipFree(*p); *p = nullptr; }
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return set_error(GP_ENOMEM, std::string("hipMalloc ") + std::to_string(count * sizeof(T)) +
+                                    " bytes: " + hipGetErrorString(e));
+  }
+  return 0;
+}
+template <class T>
+void dfree(T** p) {
+  if (*p) { (void)hipFree(*p); *p = nullptr; }
+}
+
+// graph_build.hip
+int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed);
+// gossip_engine.hip
+int finish_graph(Ctx* c);
+
+}  // namespace gp

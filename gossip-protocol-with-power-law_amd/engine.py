@@ -1,0 +1,206 @@
+"""GossipEngine: host driver of the MI355X gossip hot path over the C-ABI.
+
+Replaces, for all peers at once, the reference's per-peer threads:
+gossip_sender (Peer.py:395-408), the receive handlers (Peer.py:175-216,
+258-296), the heartbeat monitor (Peer.py:298-393) and the seed's dead-node
+removal (Seed.py:358-406).  One `round()` = liveness + injection + pull
+expansion (+ RCCL exchange on multi-GPU), all on the device.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class GossipEngine:
+    def __init__(self, device=0, **config):
+        self._lib = _lib.load()
+        self._ctx = ctypes.c_void_p()
+        check(self._lib.gp_create(int(device), ctypes.byref(self._ctx)))
+        self.device = device
+        self.cfg = _lib.Config()
+        self._lib.gp_default_config(ctypes.byref(self.cfg))
+        self.n = 0
+        self.m = 0
+        self.words = 0
+        self.origin = None
+        self.inject_round = None
+        if config:
+            self.configure(**config)
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self):
+        if self._ctx:
+            self._lib.gp_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def configure(self, **kw):
+        for k, v in kw.items():
+            if not hasattr(self.cfg, k):
+                raise KeyError(f"unknown config field {k}")
+            setattr(self.cfg, k, v)
+        check(self._lib.gp_configure(self._ctx, ctypes.byref(self.cfg)))
+
+    # -- overlay -----------------------------------------------------------
+    def load_graph(self, csr):
+        rp = np.ascontiguousarray(csr.row_ptr, dtype=np.int64)
+        col = np.ascontiguousarray(csr.col, dtype=np.int32)
+        check(self._lib.gp_load_graph(self._ctx, int(csr.n), int(col.size), _ptr(rp), _ptr(col),
+                                      1 if csr.directed else 0, None, None))
+        self.n = int(csr.n)
+
+    def build_chung_lu(self, n, dbar, gamma, seed):
+        check(self._lib.gp_build_chung_lu(self._ctx, int(n), float(dbar), float(gamma), int(seed)))
+        self.n = int(n)
+
+    def graph(self):
+        from .overlay import CSR
+        n, nnz = self.info()[:2]
+        rp = np.empty(n + 1, dtype=np.int64)
+        col = np.empty(nnz, dtype=np.int32)
+        check(self._lib.gp_read(self._ctx, _lib.ROW_PTR, _ptr(rp), rp.nbytes))
+        check(self._lib.gp_read(self._ctx, _lib.COL, _ptr(col), col.nbytes))
+        return CSR(n, rp, col, False)
+
+    def info(self):
+        n, nnz = ctypes.c_int64(), ctypes.c_int64()
+        m, w = ctypes.c_int32(), ctypes.c_int32()
+        check(self._lib.gp_info(self._ctx, ctypes.byref(n), ctypes.byref(nnz), ctypes.byref(m), ctypes.byref(w)))
+        return n.value, nnz.value, m.value, w.value
+
+    # -- partition / RCCL --------------------------------------------------
+    def set_partition(self, rank, nranks):
+        check(self._lib.gp_set_partition(self._ctx, int(rank), int(nranks)))
+
+    def partition(self):
+        b, e = ctypes.c_int64(), ctypes.c_int64()
+        check(self._lib.gp_get_partition(self._ctx, ctypes.byref(b), ctypes.byref(e)))
+        return b.value, e.value
+
+    @staticmethod
+    def comm_unique_id():
+        buf = ctypes.create_string_buffer(128)
+        check(_lib.load().gp_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, unique_id, nranks, rank):
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        check(self._lib.gp_comm_init(self._ctx, buf, int(nranks), int(rank)))
+
+    # -- messages / run ----------------------------------------------------
+    def set_messages(self, origin, inject_round=None):
+        o = np.ascontiguousarray(origin, dtype=np.int32)
+        r = None if inject_round is None else np.ascontiguousarray(inject_round, dtype=np.int32)
+        if r is not None and r.shape != o.shape:
+            raise ValueError("origin and inject_round differ in length")
+        check(self._lib.gp_set_messages(self._ctx, int(o.size), _ptr(o), _ptr(r)))
+        self.origin = o
+        self.inject_round = r if r is not None else np.zeros_like(o)
+        _, _, self.m, self.words = self.info()
+
+    def reset(self):
+        check(self._lib.gp_reset(self._ctx))
+
+    def crash(self, verts):
+        v = np.ascontiguousarray(verts, dtype=np.int32)
+        check(self._lib.gp_crash(self._ctx, int(v.size), _ptr(v)))
+
+    def round(self):
+        st = _lib.RoundStats()
+        check(self._lib.gp_round(self._ctx, ctypes.byref(st)))
+        return st.as_dict()
+
+    @staticmethod
+    def round_group(engines):
+        """One round over single-process contexts engines[k] owning partition k
+        (device-to-device exchange, no RCCL); returns the summed counters."""
+        arr = (ctypes.c_void_p * len(engines))(*[e._ctx.value for e in engines])
+        st = _lib.RoundStats()
+        check(_lib.load().gp_round_group(arr, len(engines), ctypes.byref(st)))
+        return st.as_dict()
+
+    @staticmethod
+    def run_group(engines, max_rounds=254):
+        out = []
+        last = max(int(engines[0].inject_round.max()), 0) if engines[0].m else -1
+        for _ in range(max_rounds):
+            st = GossipEngine.round_group(engines)
+            out.append(st)
+            if st["new_bits"] == 0 and st["round"] >= last:
+                break
+        return out
+
+    def run(self, max_rounds=254):
+        buf = (_lib.RoundStats * max_rounds)()
+        k = ctypes.c_int32()
+        check(self._lib.gp_run(self._ctx, int(max_rounds), buf, ctypes.byref(k)))
+        return [buf[i].as_dict() for i in range(k.value)]
+
+    def synchronize(self):
+        check(self._lib.gp_synchronize(self._ctx))
+
+    # -- outputs -----------------------------------------------------------
+    def _read(self, what, arr):
+        check(self._lib.gp_read(self._ctx, what, _ptr(arr), arr.nbytes))
+        return arr
+
+    def nloc(self):
+        b, e = self.partition()
+        return e - b
+
+    def seen(self):
+        return self._read(_lib.SEEN, np.empty((self.nloc(), self.words), dtype=np.uint64))
+
+    def first(self):
+        return self._read(_lib.FIRST, np.empty((self.nloc(), self.m), dtype=np.uint8))
+
+    def digest(self):
+        return self._read(_lib.DIGEST, np.empty(self.nloc(), dtype=np.uint64))
+
+    def finalize(self):
+        check(self._lib.gp_finalize_messages(self._ctx))
+
+    def coverage(self):
+        return self._read(_lib.COVERAGE, np.empty(self.m, dtype=np.uint64))
+
+    def forwards(self):
+        return self._read(_lib.FORWARDS, np.empty(self.m, dtype=np.uint64))
+
+    def state(self):
+        return self._read(_lib.STATE, np.empty(self.n, dtype=np.uint8))
+
+    def miss(self):
+        return self._read(_lib.MISS, np.empty(self.n, dtype=np.uint8))
+
+    def deg_live(self):
+        return self._read(_lib.DEG_LIVE, np.empty(self.n, dtype=np.int32))
+
+    def frontier(self):
+        return self._read(_lib.FRONTIER, np.empty((self.n, self.words), dtype=np.uint64))
+
+    def reports(self, cap=1 << 20):
+        """Reports of the last round as int32 [k, 3] (dead, reporter, round),
+        unordered, plus the exact total (k < total if the buffer overflowed)."""
+        buf = np.empty((cap, 3), dtype=np.int32)
+        n = ctypes.c_int64()
+        check(self._lib.gp_reports(self._ctx, ctypes.cast(buf.ctypes.data, ctypes.POINTER(_lib.Report)),
+                                   int(cap), ctypes.byref(n)))
+        return buf[:min(n.value, cap)].copy(), n.value

@@ -1,0 +1,169 @@
+/*
+ * gossip_capi.h -- C-ABI of the MI355X gossip-propagation engine (libgossip_hip.so).
+ *
+ * The reference (Sidharthshanu/Gossip-protocol-with-power-law) has no FFI: its
+ * hot path is one OS thread per TCP socket.  This ABI replaces, for ALL peers at
+ * once, one round of
+ *   - gossip generation + fan-out         Peer.py:395-408  (gossip_sender)
+ *   - receive dispatch                    Peer.py:175-216, 258-296
+ *   - forward-once / Message-List dedup   (spec-level: absent from the reference,
+ *                                          SURVEY.md §0 finding 1)
+ *   - heartbeat liveness + dead report    Peer.py:298-393, 128-151
+ *   - seed dead-node removal              Seed.py:358-406
+ * over an overlay built by the seed registry (Seed.py:127-149) or by the
+ * degree-weighted selector (demonstrate_powerlaw.py:7-39).
+ *
+ * Conventions
+ *   - Every function returns 0 on success and a negative gp_status on failure;
+ *     gp_last_error() gives a thread-local message.  Nothing aborts or exits.
+ *   - The caller owns host arrays; they are copied in.  The context owns all
+ *     device memory.  One context = one device + one HIP stream; not thread-safe.
+ *   - Vertex ids are 0..n-1 int32; arc offsets int64.  Messages are 0..m-1 and
+ *     are packed 64 per uint64 word, W = ceil(m/64) rounded up to a power of two
+ *     (1..64 words per vertex row, i.e. m <= 4096 per context; larger message
+ *     sets are run as independent batches by the host -- messages never interact).
+ *   - Multi-GPU: one process per GPU; each context owns a contiguous vertex
+ *     slice [vbegin, vend) of equal size and exchanges frontier rows by RCCL
+ *     all-gather over xGMI after every round (gp_comm_init).
+ */
+#ifndef GOSSIP_CAPI_H
+#define GOSSIP_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GP_ABI_VERSION 1
+
+typedef struct gp_ctx gp_ctx;
+
+typedef enum gp_status {
+  GP_OK = 0,
+  GP_EINVAL = -1,     /* bad argument / shape                              */
+  GP_EHIP = -2,       /* HIP runtime error                                 */
+  GP_ENOMEM = -3,     /* device allocation failed                          */
+  GP_ESTATE = -4,     /* call out of order (e.g. round before load_graph)  */
+  GP_ERCCL = -5,      /* RCCL error                                        */
+  GP_ENOTRACK = -6    /* requested output was not tracked (see gp_config)  */
+} gp_status;
+
+/* Per-round counters (all exact integers, summed over ranks). */
+typedef struct gp_round_stats {
+  int32_t round;            /* r                                                      */
+  int32_t overflow;         /* 1 if the report buffer overflowed this round          */
+  uint64_t injected;        /* messages injected at live origins in round r          */
+  uint64_t lost;            /* messages whose origin was down at their inject round  */
+  uint64_t new_bits;        /* first receipts produced by round r (receipt round r+1)*/
+  uint64_t receivers;       /* vertices with >= 1 first receipt in round r           */
+  uint64_t sends;           /* edge-deliveries attempted in round r:
+                               sum_u deg_live(u) * |frontier_r(u)|                   */
+  uint64_t active;          /* senders with a non-empty frontier in round r          */
+  uint64_t crashed;         /* vertices that crashed in round r                      */
+  uint64_t reports;         /* "Dead Node" reports emitted in round r (Peer.py:311)  */
+  uint64_t removals;        /* vertices removed by the seed (Seed.py:387-391)        */
+  uint64_t dup_reports;     /* reports hitting "not found" (Seed.py:373-375)         */
+  uint64_t arcs_scanned;    /* in-arcs visited by the pull (byte accounting)         */
+  uint64_t rows_gathered;   /* neighbour frontier rows loaded (8*W bytes each)       */
+  uint64_t seen_rows_read;  /* receiver seen rows read (8*W bytes each)              */
+  uint64_t rows_written;    /* next rows written (+ seen rows re-written)            */
+  uint64_t vertices_visited;/* receivers whose in-list was scanned                   */
+  double expand_ms;         /* device time of the expansion kernels (HIP events)     */
+  double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
+  double round_ms;          /* device time of the whole round                        */
+} gp_round_stats;
+
+/* One dead-node report: reporter saw `dead` miss 3 heartbeats in `round`. */
+typedef struct gp_report {
+  int32_t dead;
+  int32_t reporter;
+  int32_t round;
+} gp_report;
+
+typedef struct gp_config {
+  int32_t track_first;         /* keep the u8 first-receipt matrix [n][m] (255 = never) */
+  int32_t track_digest;        /* keep per-vertex first-receipt digest u64[n]          */
+  int32_t track_msg_forwards;  /* accumulate per-message forwards every round          */
+  int32_t churn;               /* run the liveness phase every round                   */
+  double p_fail;               /* per-round crash probability of a live vertex         */
+  uint64_t churn_seed;         /* crash draws: splitmix stream        */
+  int32_t miss_threshold;      /* heartbeat misses before report (reference: 3)        */
+  int32_t hub_threshold;       /* in-degree above which a vertex is split over waves   */
+  int64_t report_capacity;     /* reports kept per round (counts stay exact)           */
+} gp_config;
+
+/* what for gp_read */
+typedef enum gp_what {
+  GP_SEEN = 0,        /* u64 [vend-vbegin][W]  owned rows of the Message-List bitmap */
+  GP_FIRST = 1,       /* u8  [vend-vbegin][m]  first-receipt round, 255 = never      */
+  GP_DIGEST = 2,      /* u64 [vend-vbegin]                                           */
+  GP_COVERAGE = 3,    /* u64 [m]  vertices holding message m (this rank's slice)     */
+  GP_FORWARDS = 4,    /* u64 [m]  sends of message m (this rank's senders)           */
+  GP_STATE = 5,       /* u8  [n]  bit0 crashed, bit1 removed                         */
+  GP_MISS = 6,        /* u8  [n]  heartbeat miss counter                             */
+  GP_DEG_LIVE = 7,    /* i32 [n]  neighbours not removed                             */
+  GP_ROW_PTR = 8,     /* i64 [n+1] in-CSR offsets (as loaded / built)                */
+  GP_COL = 9,         /* i32 [nnz] in-CSR columns                                    */
+  GP_FRONTIER = 10,   /* u64 [n][W] current frontier (rows with FPOP==0 read as 0)   */
+  GP_FPOP = 11        /* u32 [n] |frontier(v)|                                       */
+} gp_what;
+
+int gp_abi_version(void);
+const char* gp_last_error(void);
+int gp_device_count(int* n_out);
+
+int gp_create(int device, gp_ctx** out);
+void gp_destroy(gp_ctx* ctx);
+void gp_default_config(gp_config* cfg);
+int gp_configure(gp_ctx* ctx, const gp_config* cfg);
+
+/* Overlay.  In-CSR: row_ptr[v]..row_ptr[v+1] lists u with an arc u->v (the peers
+ * whose gossip v receives; Peer.py:402 sends on outgoing links).  out_degree may
+ * be NULL for undirected graphs (= in-degree).  For directed graphs the out-CSR
+ * (out_row_ptr/out_col, may be NULL when directed == 0) gives the other side of
+ * every heartbeat link for liveness reports (Peer.py:369-392 covers outgoing and
+ * incoming connections). */
+int gp_load_graph(gp_ctx* ctx, int64_t n, int64_t nnz, const int64_t* row_ptr,
+                  const int32_t* col, int32_t directed, const int64_t* out_row_ptr,
+                  const int32_t* out_col);
+
+/* Build an undirected Chung-Lu power-law overlay on the device:
+ * ~dbar*n/2 candidate edges, endpoints drawn ∝ (i+1)^(-1/(gamma-1)) with an
+ * integer alias table, self-loops dropped, de-duplicated, ids randomly relabelled. */
+int gp_build_chung_lu(gp_ctx* ctx, int64_t n, double dbar, double gamma, uint64_t seed);
+
+/* Vertex slice owned by this context (default: all). */
+int gp_set_partition(gp_ctx* ctx, int32_t rank, int32_t nranks);
+int gp_get_partition(gp_ctx* ctx, int64_t* vbegin, int64_t* vend);
+
+/* RCCL: rank 0 calls gp_comm_unique_id, the host distributes the 128 bytes. */
+int gp_comm_unique_id(void* out128);
+int gp_comm_init(gp_ctx* ctx, const void* unique_id128, int32_t nranks, int32_t rank);
+
+/* Messages: origin vertex and inject round of each message (Peer.py:397-399:
+ * message #n of a peer is its n-th generated gossip). */
+int gp_set_messages(gp_ctx* ctx, int32_t m, const int32_t* origin, const int32_t* inject_round);
+
+/* Explicit crash injection (the reference's silent mode, Peer.py:437-439),
+ * applied at the start of the next round in addition to random churn. */
+int gp_crash(gp_ctx* ctx, int32_t nverts, const int32_t* verts);
+
+int gp_reset(gp_ctx* ctx);                       /* new run: clear all per-run state */
+int gp_round(gp_ctx* ctx, gp_round_stats* out);  /* liveness + injection + expansion */
+int gp_run(gp_ctx* ctx, int32_t max_rounds, gp_round_stats* per_round, int32_t* rounds_out);
+/* Single-process multi-context round: ctxs[k] owns partition k of nctx (same or
+ * different devices, no RCCL); the exchange is device-to-device copies and the
+ * counters are summed into *out.  Used for partition-invariance checks on one GPU. */
+int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out);
+int gp_finalize_messages(gp_ctx* ctx);           /* per-message coverage/forwards    */
+int gp_read(gp_ctx* ctx, int32_t what, void* host, int64_t bytes);
+int gp_reports(gp_ctx* ctx, gp_report* buf, int64_t cap, int64_t* n_out);
+int gp_synchronize(gp_ctx* ctx);
+int gp_info(gp_ctx* ctx, int64_t* n, int64_t* nnz, int32_t* m, int32_t* words);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GOSSIP_CAPI_H */

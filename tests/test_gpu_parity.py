@@ -1,0 +1,226 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle.
+
+Bar: bit-exact for everything -- first-receipt matrices, per-vertex digests,
+Message-List bitmaps, per-message coverage/forwards, per-round counters,
+dead-node reports (as sets), vertex state.  Oracles: oracle/gossip_oracle.c
+(cross-checked against the per-peer sha256 harness in test_oracle.py) and the
+reference's own fixtures in tests/golden/.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+STAT_KEYS = ("injected", "lost", "new_bits", "receivers", "sends", "active", "crashed",
+             "reports", "removals", "dup_reports")
+
+
+def _engine(pkg, g, origin, inject=None, **cfg):
+    eng = pkg.GossipEngine(0, **cfg)
+    eng.load_graph(g)
+    eng.set_messages(origin, inject)
+    eng.reset()
+    return eng
+
+
+def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096, **kw):
+    churn = kw.get("churn", False)
+    cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(bool(churn or crashes)),
+               churn=int(churn), p_fail=kw.get("p_fail", 0.0), churn_seed=kw.get("churn_seed", 0),
+               hub_threshold=hub_threshold)
+    eng = _engine(pkg, g, origin, inject, **cfg)
+    by_round = {}
+    for v, r in crashes:
+        by_round.setdefault(r, []).append(v)
+    stats, reports = [], []
+    last = int(np.max(inject)) if inject is not None and len(inject) else 0
+    for r in range(254):
+        if r in by_round:
+            eng.crash(by_round[r])
+        st = eng.round()
+        stats.append(st)
+        rep, nrep = eng.reports()
+        assert nrep == len(rep)
+        reports.extend(map(tuple, rep.tolist()))
+        if st["new_bits"] == 0 and r >= last:
+            break
+    eng.finalize()
+    ref = oracle.run(g, origin, inject, crashes=crashes, want_first=first, **kw)
+    assert len(stats) == ref["rounds"]
+    for a, b in zip(stats, ref["stats"]):
+        for k in STAT_KEYS:
+            assert a[k] == b[k], (k, a["round"], a[k], b[k])
+    W = eng.words
+    assert np.array_equal(eng.seen(), ref["seen"][:, :W])
+    if first:
+        assert np.array_equal(eng.first(), ref["first"])
+    assert np.array_equal(eng.digest(), ref["digest"])
+    assert np.array_equal(eng.coverage(), ref["coverage"])
+    assert np.array_equal(eng.forwards(), ref["forwards"])
+    assert sorted(reports) == sorted(map(tuple, ref["reports"].tolist()))
+    out = {"stats": stats, "eng": eng, "ref": ref}
+    return out
+
+
+def test_c2_ba_10k_64(pkg, oracle):
+    """BASELINE config 2: 10^4-node BA(m=2), 64 concurrent messages."""
+    g = pkg.overlay.barabasi_albert(10_000, 2, seed=2)
+    origin = pkg.overlay.random_origins(g.n, 64, seed=2)
+    r = _compare(pkg, oracle, g, origin)
+    total = sum(s["sends"] for s in r["stats"])
+    assert total == 64 * g.nnz   # connected BA: every message crosses every arc once
+    r["eng"].close()
+
+
+@pytest.mark.parametrize("m", [1, 10, 63, 64, 65, 130, 300, 1000, 4096])
+def test_message_widths(pkg, oracle, m):
+    g = pkg.overlay.barabasi_albert(1500, 3, seed=m)
+    origin = pkg.overlay.random_origins(g.n, m, seed=m)
+    inject = (np.arange(m) % 5).astype(np.int32)
+    _compare(pkg, oracle, g, origin, inject)["eng"].close()
+
+
+def test_hub_split(pkg, oracle):
+    """Force the multi-wave hub path (partials + final) on every vertex above 64 arcs."""
+    rp, col = oracle.chung_lu(20_000, 8, 2.2, 11)
+    g = pkg.CSR(20_000, rp, col, False)
+    assert np.diff(rp).max() > 1000
+    origin = pkg.overlay.random_origins(g.n, 256, seed=11)
+    _compare(pkg, oracle, g, origin, hub_threshold=64)["eng"].close()
+
+
+def test_c1_directed_schedule_and_direct_deliveries(pkg, oracle):
+    """C1: 10 peers, first-3 overlay, 10 msgs/peer every 5 rounds.  Round 1 after
+    each injection reproduces the reference's direct delivery matrix."""
+    golden = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "c1_wire.json")))
+    g = pkg.overlay.first3_overlay(10)
+    origin, inject, count = pkg.peer.c1_schedule(10)
+    origin, inject = np.array(origin, np.int32), np.array(inject, np.int32)
+    r = _compare(pkg, oracle, g, origin, inject)
+    first = r["eng"].first()
+    direct = sorted([int(origin[k]), int(count[k]), int(v)] for k in range(len(origin))
+                    for v in np.nonzero(first[:, k] == inject[k] + 1)[0])
+    assert direct == sorted(golden["deliveries"])
+    r["eng"].close()
+
+
+def test_churn_random(pkg, oracle):
+    g = pkg.overlay.barabasi_albert(5000, 2, seed=5)
+    origin = pkg.overlay.random_origins(g.n, 128, seed=5)
+    inject = (np.arange(128) % 9).astype(np.int32)
+    r = _compare(pkg, oracle, g, origin, inject, churn=True, p_fail=0.03, churn_seed=77)
+    assert sum(s["removals"] for s in r["stats"]) > 0
+    r["eng"].close()
+
+
+def test_explicit_crashes_directed(pkg, oracle):
+    g = pkg.overlay.first3_overlay(10)
+    origin, inject, _ = pkg.peer.c1_schedule(10)
+    r = _compare(pkg, oracle, g, np.array(origin, np.int32), np.array(inject, np.int32),
+                 crashes=[(4, 1), (0, 6), (9, 3)])
+    assert sum(s["removals"] for s in r["stats"]) >= 2
+    r["eng"].close()
+
+
+def test_chung_lu_device_builder_matches_oracle(pkg, oracle):
+    for n, dbar, seed in [(1000, 4, 1), (100_000, 8, 3)]:
+        with pkg.GossipEngine(0) as eng:
+            eng.build_chung_lu(n, dbar, 2.5, seed)
+            dg = eng.graph()
+        rp, col = oracle.chung_lu(n, dbar, 2.5, seed)
+        assert np.array_equal(dg.row_ptr, rp)
+        assert np.array_equal(dg.col, col)
+
+
+def test_c3_chung_lu_1e6_1024(pkg, oracle):
+    """BASELINE config 3: 10^6-node Chung-Lu (gamma 2.5), 1024 messages."""
+    n = 1_000_000
+    with pkg.GossipEngine(0, track_digest=1) as eng:
+        eng.build_chung_lu(n, 8, 2.5, 3)
+        g = eng.graph()
+        origin = pkg.overlay.random_origins(n, 1024, seed=3)
+        eng.set_messages(origin)
+        eng.reset()
+        stats = eng.run()
+        eng.finalize()
+        digest, cov, fwd = eng.digest(), eng.coverage(), eng.forwards()
+    ref = oracle.run(g, origin, nthreads=8, want_first=False)
+    assert len(stats) == ref["rounds"]
+    for a, b in zip(stats, ref["stats"]):
+        for k in STAT_KEYS:
+            assert a[k] == b[k], (k, a["round"])
+    assert np.array_equal(digest, ref["digest"])
+    assert np.array_equal(cov, ref["coverage"])
+    assert np.array_equal(fwd, ref["forwards"])
+
+
+def test_group_partition_invariance(pkg, oracle):
+    """2 and 3 contexts on one GPU (device-to-device exchange) == 1 context."""
+    g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
+    origin = pkg.overlay.random_origins(g.n, 200, seed=8)
+    inject = (np.arange(200) % 4).astype(np.int32)
+    ref = oracle.run(g, origin, inject, churn=True, p_fail=0.02, churn_seed=3, want_first=True)
+    for P in (2, 3):
+        engs = []
+        for k in range(P):
+            e = pkg.GossipEngine(0, track_first=1, churn=1, p_fail=0.02, churn_seed=3, track_msg_forwards=1)
+            e.load_graph(g)
+            e.set_partition(k, P)
+            e.set_messages(origin, inject)
+            e.reset()
+            engs.append(e)
+        stats = pkg.GossipEngine.run_group(engs)
+        assert len(stats) == ref["rounds"]
+        for a, b in zip(stats, ref["stats"]):
+            for k in STAT_KEYS:
+                assert a[k] == b[k], (P, k, a["round"])
+        first = np.concatenate([e.first() for e in engs])
+        digest = np.concatenate([e.digest() for e in engs])
+        assert np.array_equal(first, ref["first"])
+        assert np.array_equal(digest, ref["digest"])
+        cov = fwd = 0
+        for e in engs:
+            e.finalize()
+            cov = cov + e.coverage()
+            fwd = fwd + e.forwards()
+        assert np.array_equal(cov, ref["coverage"])
+        assert np.array_equal(fwd, ref["forwards"])
+        for e in engs:
+            e.close()
+
+
+def test_edge_cases(pkg, oracle):
+    # isolated vertices, a single message, origin that crashes before injection
+    g = pkg.CSR.from_edges(50, [(0, 1), (1, 2), (2, 3), (10, 11)])
+    _compare(pkg, oracle, g, np.array([0], np.int32))["eng"].close()
+    _compare(pkg, oracle, g, np.array([7, 7, 7], np.int32))["eng"].close()
+    _compare(pkg, oracle, g, np.array([0, 10, 2], np.int32), np.array([0, 2, 4], np.int32),
+             crashes=[(10, 1)])["eng"].close()
+    # all messages at one origin of a star (hub receives nothing new after round 1)
+    star = pkg.CSR.from_edges(200, [(0, i) for i in range(1, 200)])
+    _compare(pkg, oracle, star, np.full(100, 5, np.int32), hub_threshold=64)["eng"].close()
+
+
+def test_full_size_invariants_c3(pkg):
+    """Size-independent properties at a large size: conservation of sends and
+    receipts, idempotence of a repeated run."""
+    n, m = 1 << 20, 4096
+    with pkg.GossipEngine(0, track_digest=1) as eng:
+        eng.build_chung_lu(n, 16, 2.5, 4)
+        origin = pkg.overlay.random_origins(n, m, seed=4)
+        eng.set_messages(origin)
+        eng.reset()
+        s1 = eng.run()
+        d1 = eng.digest().copy()
+        eng.finalize()
+        cov, fwd = eng.coverage(), eng.forwards()
+        eng.reset()
+        s2 = eng.run()
+        d2 = eng.digest()
+    assert np.array_equal(d1, d2)
+    assert [x["new_bits"] for x in s1] == [x["new_bits"] for x in s2]
+    assert sum(x["sends"] for x in s1) == int(fwd.sum())
+    assert sum(x["new_bits"] + x["injected"] for x in s1) == int(cov.sum())
