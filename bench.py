@@ -46,32 +46,6 @@ def parse():
     return ap.parse_args()
 
 
-def dist_setup(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    pg = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        pg = dist
-    return world, rank, local, pg
-
-
-def barrier(pg):
-    if pg is not None:
-        pg.barrier()
-
-
-def allmax(pg, x):
-    if pg is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
-
-
 def round_bytes(st, words, nloc):
     """Algorithmic bytes of one expansion launch of the sparse-aware pull
     (DESIGN.md §4): per owned vertex 21 B of vertex state, per scanned arc 8 B
@@ -107,9 +81,11 @@ def cpu_baseline(args, eng, origin, pkg):
 
 def main():
     args = parse()
-    world, rank, local, pg = dist_setup(args)
     import _gossip_pkg
     pkg = _gossip_pkg.load()
+    dist = pkg.dist
+    world, rank, local = dist.env()
+    pg = dist.init("gloo")
     n = 1 << args.log2n
     eng = pkg.GossipEngine(local, track_digest=1, track_first=0, hub_threshold=args.hub_threshold)
     t0 = time.perf_counter()
@@ -117,13 +93,11 @@ def main():
     _, nnz, _, _ = eng.info()
     if world > 1:
         eng.set_partition(rank, world)
-        uid = [pkg.GossipEngine.comm_unique_id() if rank == 0 else None]
-        pg.broadcast_object_list(uid, src=0)
-        eng.comm_init(uid[0], world, rank)
+        eng.comm_init(dist.share_comm_id(pg, pkg.GossipEngine.comm_unique_id), world, rank)
     origin = pkg.overlay.random_origins(n, args.messages, seed=args.seed)
     eng.set_messages(origin)
     setup_s = time.perf_counter() - t0
-    vb, ve = eng.partition()
+
 
     def step():
         eng.reset()
@@ -131,20 +105,22 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    barrier(pg)
+    if pg is not None:
+        pg.barrier()
     eng.synchronize()
     t0 = time.perf_counter()
     runs = [step() for _ in range(args.steps)]
     eng.synchronize()
-    barrier(pg)
-    dt = allmax(pg, time.perf_counter() - t0)
+    if pg is not None:
+        pg.barrier()
+    dt = dist.allmax(pg, time.perf_counter() - t0)
 
     sends = sum(s["sends"] for r in runs for s in r)   # global (all-reduced) counters
     rounds = sum(len(r) for r in runs)
     exp_ms = sum(s["expand_ms"] for r in runs for s in r)
     exch_ms = sum(s["exchange_ms"] for r in runs for s in r)
-    nbytes = sum(round_bytes(s, eng.words, ve - vb) for r in runs for s in r)
-    if world > 1:   # byte counters are global: per-rank share for the per-GPU roofline
+    nbytes = sum(round_bytes(s, eng.words, n) for r in runs for s in r)
+    if world > 1:   # counters are global (all-reduced): per-rank share for the per-GPU roofline
         nbytes /= world
     achieved = nbytes / (exp_ms * 1e-3) / 1e9 if exp_ms > 0 else 0.0
     dense_eq = dense_round_bytes(n, nnz, eng.words) * rounds / world / (exp_ms * 1e-3) / 1e9

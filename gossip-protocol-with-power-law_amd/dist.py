@@ -1,0 +1,75 @@
+"""Multi-process (one process per GPU) host orchestration.
+
+The data path is RCCL inside libgossip_hip.so (all-gather of the owned next rows
+over xGMI every round); torch.distributed (gloo, CPU) is only the control plane:
+it hands rank 0's RCCL unique id to every rank, aligns the timed region and
+gathers per-rank outputs (the owned slices) for checking.
+
+Partition: rank p owns the contiguous vertex slice [p*S, min((p+1)*S, n)) with
+S = ceil(n / nranks) -- equal-size slices as RCCL's all-gather requires; the
+overlay ids are randomly relabelled, so equal slices carry
+statistically equal arc counts.
+"""
+import os
+
+import numpy as np
+
+
+def env():
+    """(world_size, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def partition_bounds(n, nranks):
+    s = (n + nranks - 1) // nranks
+    return [(min(n, p * s), min(n, (p + 1) * s)) for p in range(nranks)]
+
+
+def init(backend="gloo"):
+    import torch.distributed as dist
+    world, rank, _ = env()
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    return dist if world > 1 else None
+
+
+def broadcast_bytes(pg, data, src=0):
+    if pg is None:
+        return data
+    box = [data if pg.get_rank() == src else None]
+    pg.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+def share_comm_id(pg, make_id):
+    """Rank 0 creates the RCCL unique id (128 bytes); every rank receives it."""
+    rank = pg.get_rank() if pg is not None else 0
+    return broadcast_bytes(pg, make_id() if rank == 0 else None)
+
+
+def gather_slices(pg, local):
+    """Concatenate the ranks' owned slices in rank order (all ranks get it)."""
+    if pg is None:
+        return local
+    parts = [None] * pg.get_world_size()
+    pg.all_gather_object(parts, np.asarray(local))
+    return np.concatenate(parts)
+
+
+def allsum(pg, x):
+    if pg is None:
+        return x
+    import torch
+    t = torch.as_tensor(np.asarray(x, dtype=np.float64))
+    pg.all_reduce(t)
+    return t.numpy()
+
+
+def allmax(pg, x):
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())

@@ -1,0 +1,72 @@
+"""Multi-process host orchestration on CPU (gloo, world size 2): RCCL-id
+hand-off, partition bounds, ordered gather of owned slices, counter sums.
+The per-rank compute is the CPU oracle on the full overlay, sliced as the
+engine slices it; the device exchange itself is covered on the GPU by
+test_gpu_parity.py::test_group_partition_invariance."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import _gossip_pkg
+    from oracle import lib as oracle
+    pkg = _gossip_pkg.load()
+    d = pkg.dist
+    pg = d.init("gloo")
+    try:
+        uid = d.share_comm_id(pg, lambda: bytes(range(128)))
+        g = pkg.overlay.barabasi_albert(1001, 2, seed=3)
+        origin = pkg.overlay.random_origins(g.n, 100, 3)
+        ref = oracle.run(g, origin, want_first=True)
+        vb, ve = d.partition_bounds(g.n, world)[rank]
+        first = d.gather_slices(pg, ref["first"][vb:ve])
+        digest = d.gather_slices(pg, ref["digest"][vb:ve])
+        cov_local = (ref["first"][vb:ve] != 255).sum(axis=0)
+        cov = d.allsum(pg, cov_local)
+        tmax = d.allmax(pg, float(rank))
+        q.put((rank, uid == bytes(range(128)), np.array_equal(first, ref["first"]),
+               np.array_equal(digest, ref["digest"]), np.array_equal(cov, ref["coverage"]), tmax))
+    finally:
+        pg.destroy_process_group()
+
+
+def test_two_rank_gloo_orchestration():
+    mp = pytest.importorskip("torch.multiprocessing")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, uid_ok, first_ok, dig_ok, cov_ok, tmax in res:
+        assert uid_ok and first_ok and dig_ok and cov_ok and tmax == 1.0
+
+
+def test_partition_bounds(pkg):
+    d = pkg.dist
+    for n, p in [(10, 3), (1 << 24, 8), (7, 8), (1000, 1)]:
+        b = d.partition_bounds(n, p)
+        assert b[0][0] == 0 and b[-1][1] == n
+        assert all(b[i][1] == b[i + 1][0] for i in range(p - 1))
+        s = (n + p - 1) // p
+        assert all(e - s0 <= s for s0, e in b)
