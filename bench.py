@@ -38,6 +38,10 @@ def parse():
     ap.add_argument("--messages", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--hub-threshold", type=int, default=4096)
+    ap.add_argument("--hot-degree", type=int, default=0,
+                    help="cache-steer rows of vertices with in-degree >= this (0 = off)")
+    ap.add_argument("--push-ratio", type=float, default=40.0)
+    ap.add_argument("--early-exit", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-messages", type=int, default=64)
@@ -87,7 +91,9 @@ def main():
     world, rank, local = dist.env()
     pg = dist.init("gloo")
     n = 1 << args.log2n
-    eng = pkg.GossipEngine(local, track_digest=1, track_first=0, hub_threshold=args.hub_threshold)
+    eng = pkg.GossipEngine(local, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
+                           hot_degree=args.hot_degree, push_ratio=args.push_ratio,
+                           early_exit=args.early_exit)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()
@@ -126,9 +132,9 @@ def main():
     dense_eq = dense_round_bytes(n, nnz, eng.words) * rounds / world / (exp_ms * 1e-3) / 1e9
     if args.profile_steps and rank == 0:
         for s in runs[-1]:
-            print(json.dumps({k: s[k] for k in ("round", "new_bits", "sends", "active", "receivers",
+            print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
-                                                "rows_written", "expand_ms", "exchange_ms")}),
+                                                "rows_written", "atomics", "expand_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

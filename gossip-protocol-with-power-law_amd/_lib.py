@@ -45,6 +45,10 @@ class RoundStats(ctypes.Structure):
         ("seen_rows_read", ctypes.c_uint64),
         ("rows_written", ctypes.c_uint64),
         ("vertices_visited", ctypes.c_uint64),
+        ("atomics", ctypes.c_uint64),
+        ("next_arcs", ctypes.c_uint64),
+        ("mode", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
         ("expand_ms", ctypes.c_double),
         ("exchange_ms", ctypes.c_double),
         ("round_ms", ctypes.c_double),
@@ -69,6 +73,9 @@ class Config(ctypes.Structure):
         ("miss_threshold", ctypes.c_int32),
         ("hub_threshold", ctypes.c_int32),
         ("report_capacity", ctypes.c_int64),
+        ("push_ratio", ctypes.c_double),
+        ("early_exit", ctypes.c_int32),
+        ("hot_degree", ctypes.c_int32),
     ]
 
 

@@ -41,7 +41,6 @@ typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 constexpr int BLOCK = 256;         // 4 waves
 constexpr int WAVES = BLOCK / 64;
 constexpr int NPART = 2048;        // partial stat slots (spread the atomics)
-constexpr int NST = 16;            // stats kept per partial slot (slots 0..15)
 
 // ---------------------------------------------------------------------------
 // geometry: a wave loads 16 B per lane -> W/2 lanes per row, 128/W rows per
@@ -64,6 +63,34 @@ __device__ __forceinline__ u64x2 load_piece(const u64* __restrict__ base, int64_
     return r;
   }
 }
+// non-temporal forms: streamed data that must not displace the hub rows the
+// gather re-reads from the Infinity Cache / L2
+template <int W>
+__device__ __forceinline__ u64x2 load_piece_nt(const u64* __restrict__ base, int64_t row, int lw) {
+  if constexpr (W >= 2) {
+    return __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(base + row * W + lw * 2));
+  } else {
+    u64x2 r;
+    r.x = __builtin_nontemporal_load(base + row);
+    r.y = 0;
+    return r;
+  }
+}
+template <int W>
+__device__ __forceinline__ void store_piece_nt(u64* __restrict__ base, int64_t row, int lw, u64x2 x) {
+  if constexpr (W >= 2) {
+    __builtin_nontemporal_store(x, reinterpret_cast<u64x2*>(base + row * W + lw * 2));
+  } else {
+    __builtin_nontemporal_store(x.x, base + row);
+  }
+}
+template <int W>
+__device__ __forceinline__ u64x2 load_row(const u64* __restrict__ base, int32_t tagged, int lw, bool steer) {
+  const int32_t u = tagged & 0x7FFFFFFF;
+  if (steer && tagged >= 0) return load_piece_nt<W>(base, u, lw);   // cold row
+  return load_piece<W>(base, u, lw);                                  // hub row: cacheable
+}
+
 template <int W>
 __device__ __forceinline__ void store_piece(u64* __restrict__ base, int64_t row, int lw, u64x2 x) {
   if constexpr (W >= 2) {
@@ -110,25 +137,25 @@ __device__ void flush_stats(const WaveStats& s, u64* __restrict__ partial) {
     u64 t = 0;
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) t += red[w][threadIdx.x];
-    if (t) atomicAdd(&partial[(size_t)(blockIdx.x % NPART) * NST + threadIdx.x], t);
+    if (t) atomicAdd(&partial[(size_t)threadIdx.x * NPART + (blockIdx.x % NPART)], t);
   }
 }
+// partial layout [slot][NPART]: block k sums slot k with one coalesced sweep
 __global__ void k_stats_reduce(u64* __restrict__ partial, u64* __restrict__ stats) {
-  // one block of 256 threads; thread t sums slot (t % NST) over a strided part
   __shared__ u64 acc[BLOCK];
-  const int k = threadIdx.x % NST, lane_grp = threadIdx.x / NST;   // 16 groups
+  const int k = blockIdx.x;
   u64 t = 0;
-  for (int p = lane_grp; p < NPART; p += BLOCK / NST) {
-    t += partial[(size_t)p * NST + k];
-    partial[(size_t)p * NST + k] = 0;
+  for (int p = threadIdx.x; p < NPART; p += BLOCK) {
+    t += partial[(size_t)k * NPART + p];
+    partial[(size_t)k * NPART + p] = 0;
   }
   acc[threadIdx.x] = t;
   __syncthreads();
-  if (threadIdx.x < NST) {
-    u64 s = 0;
-    for (int g = 0; g < BLOCK / NST; ++g) s += acc[g * NST + threadIdx.x];
-    stats[threadIdx.x] += s;
+  for (int w = BLOCK / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) acc[threadIdx.x] += acc[threadIdx.x + w];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) stats[k] += acc[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -138,6 +165,13 @@ struct ExpandArgs {
   const int32_t* __restrict__ col;
   const u64* __restrict__ front;       // frontier_r
   const uint32_t* __restrict__ fpop;   // |frontier_r|
+  const u64* __restrict__ abits;       // bit v: frontier_r(v) != 0 (2 MB at 2^24: L2-resident)
+  const int32_t* __restrict__ gcol;    // in-CSR columns in gather order (neighbour degree desc)
+  const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
+  const u64* __restrict__ cmask;       // [K][W] messages originating in each component
+  int32_t early_exit;                  // this round scans with the coverage check
+  int32_t steer;                       // nt loads/stores for streamed data, cached hub rows
+  const uint32_t* __restrict__ done_at;// |messages of v's component|: seenpop == done_at -> done
   u64* __restrict__ next;
   uint32_t* __restrict__ fpop_next;
   u64* __restrict__ seen;
@@ -152,6 +186,15 @@ struct ExpandArgs {
   const int32_t* __restrict__ hub_item_ptr;
   u64* __restrict__ hub_partial;
   uint32_t* __restrict__ hub_pnz;
+  // push mode
+  const int64_t* __restrict__ orp;     // out-CSR (undirected: == row_ptr/col)
+  const int32_t* __restrict__ ocol;
+  u64* __restrict__ acc;               // [n_alloc][W] OR accumulator (all-zero between uses)
+  int32_t* __restrict__ touch;         // [n_alloc] last round v was pushed to
+  int32_t* __restrict__ touched;       // receivers touched this round
+  const int32_t* __restrict__ active;  // senders with deg <= hub_thr
+  const int32_t* __restrict__ big;     // senders with deg > hub_thr
+  u64* __restrict__ stats;             // device counters (cursors)
   int64_t vbegin, nloc;
   int64_t n_items;                     // hub items / hubs for the hub kernels
   int32_t m_total;
@@ -159,46 +202,6 @@ struct ExpandArgs {
   int32_t hub_thr;
   int32_t vpw;                         // vertices per wave (k_expand)
 };
-
-// OR the frontier rows of the active in-neighbours in arcs [b, e) into acc.
-// Neighbour ids are staged in LDS 64 at a time, compacted to the active ones.
-template <int W>
-__device__ __forceinline__ void gather(const ExpandArgs& a, int64_t b, int64_t e,
-                                       int32_t* __restrict__ sidx, int lane, int g, int lw,
-                                       u64x2& acc, WaveStats& st) {
-  constexpr int RPI = Geo<W>::RPI;
-  for (int64_t j0 = b; j0 < e; j0 += 64) {
-    const int n = (int)min((int64_t)64, e - j0);
-    int u = -1;
-    if (lane < n) u = a.col[j0 + lane];
-    const bool act = (u >= 0) && (a.fpop[u] != 0u);
-    const u64 mask = __ballot(act);
-    const int cnt = __popcll(mask);
-    st.c[S_ARCS] += n;
-    st.c[S_GATHERED] += cnt;
-    if (cnt == 0) continue;
-    if (act) sidx[lane_rank(mask)] = u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int k = g; k < cnt; k += 4 * RPI) {
-      const int k1 = k + RPI, k2 = k + 2 * RPI, k3 = k + 3 * RPI;
-      const int u0 = sidx[k];
-      const int u1 = k1 < cnt ? sidx[k1] : -1;
-      const int u2 = k2 < cnt ? sidx[k2] : -1;
-      const int u3 = k3 < cnt ? sidx[k3] : -1;
-      u64x2 r0 = load_piece<W>(a.front, u0, lw);
-      u64x2 r1 = {0, 0}, r2 = {0, 0}, r3 = {0, 0};
-      if (u1 >= 0) r1 = load_piece<W>(a.front, u1, lw);
-      if (u2 >= 0) r2 = load_piece<W>(a.front, u2, lw);
-      if (u3 >= 0) r3 = load_piece<W>(a.front, u3, lw);
-      acc |= (r0 | r1) | (r2 | r3);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-}
 
 // OR-reduce the row slots of the wave: afterwards every lane holds the full
 // result for its lw column.
@@ -209,6 +212,65 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
   for (int s = LPR; s < 64; s <<= 1) {
     acc.x |= __shfl_xor(acc.x, s);
     if constexpr (W >= 2) acc.y |= __shfl_xor(acc.y, s);
+  }
+}
+
+// OR the frontier rows of the active in-neighbours in arcs [b, e) into acc.
+// Neighbour ids come 64 at a time from the gather-order CSR (in-lists sorted
+// by neighbour degree, hubs first), are filtered by the L2-resident activity
+// bitmap and staged in LDS compacted to the active ones.
+// Early exit (bottom-up, Beamer et al. SC'12): with `ee` the wave stops once
+// acc | seen covers every message of the vertex's component (cm) -- group-0
+// lanes hold the seen (sv) and mask (cm) pieces.  OR is idempotent, so
+// acc & ~seen is exactly what the full scan would give.
+template <int W>
+__device__ __forceinline__ void gather(const ExpandArgs& a, int64_t b, int64_t e,
+                                       int32_t* __restrict__ sidx, int lane, int g, int lw,
+                                       u64x2& acc, WaveStats& st, bool ee, u64x2 sv, u64x2 cm) {
+  constexpr int RPI = Geo<W>::RPI;
+  for (int64_t j0 = b; j0 < e; j0 += 64) {
+    const int n = (int)min((int64_t)64, e - j0);
+    int32_t tu = 0;   // column id, bit 31 = hub row (cache-steered)
+    bool act = false;
+    if (lane < n) {
+      tu = a.steer ? __builtin_nontemporal_load(a.gcol + j0 + lane) : a.gcol[j0 + lane];
+      const int32_t u = tu & 0x7FFFFFFF;
+      act = (a.abits[u >> 6] >> (u & 63)) & 1ull;
+    }
+    const u64 mask = __ballot(act);
+    const int cnt = __popcll(mask);
+    st.c[S_ARCS] += n;
+    if (cnt == 0) continue;
+    if (act) sidx[lane_rank(mask)] = tu;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bool stop = false;
+    for (int k0 = 0; k0 < cnt; k0 += 4 * RPI) {
+      const int k = k0 + g, k1 = k + RPI, k2 = k + 2 * RPI, k3 = k + 3 * RPI;
+      const bool steer = a.steer != 0;
+      u64x2 r0 = {0, 0}, r1 = {0, 0}, r2 = {0, 0}, r3 = {0, 0};
+      if (k < cnt) r0 = load_row<W>(a.front, sidx[k], lw, steer);
+      if (k1 < cnt) r1 = load_row<W>(a.front, sidx[k1], lw, steer);
+      if (k2 < cnt) r2 = load_row<W>(a.front, sidx[k2], lw, steer);
+      if (k3 < cnt) r3 = load_row<W>(a.front, sidx[k3], lw, steer);
+      acc |= (r0 | r1) | (r2 | r3);
+      st.c[S_GATHERED] += (u64)min(4 * RPI, cnt - k0);
+      if (ee) {
+        u64x2 t = acc;
+        reduce_slots<W>(t);
+        u64x2 miss = {0, 0};
+        if (g == 0) miss = cm & ~(t | sv);
+        if (!__any((miss.x | miss.y) != 0ull)) {
+          stop = true;
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (stop) break;
   }
 }
 
@@ -234,17 +296,18 @@ __device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int w
 // receiver side of vertex v (local index i): apply seen, write next, counters
 template <int W>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
-                                           int g, int lw, WaveStats& st) {
+                                           int g, int lw, WaveStats& st, bool have_sv = false,
+                                           u64x2 sv_pre = u64x2{0, 0}) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
     if (lane == 0) a.fpop_next[v] = 0;
     return;
   }
-  st.c[S_SEEN_READ] += 1;
+  if (!have_sv) st.c[S_SEEN_READ] += 1;
   u64x2 sv = {0, 0}, nw = {0, 0};
   if (g == 0) {
-    sv = load_piece<W>(a.seen, i, lw);
+    sv = have_sv ? sv_pre : (a.steer ? load_piece_nt<W>(a.seen, i, lw) : load_piece<W>(a.seen, i, lw));
     nw = acc & ~sv;
   }
   const uint32_t pc = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
@@ -254,8 +317,13 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
     return;
   }
   if (g == 0) {
-    store_piece<W>(a.next, v, lw, nw);
-    if (nw.x | nw.y) store_piece<W>(a.seen, i, lw, sv | nw);
+    if (a.steer) {
+      store_piece_nt<W>(a.next, v, lw, nw);
+      if (nw.x | nw.y) store_piece_nt<W>(a.seen, i, lw, sv | nw);
+    } else {
+      store_piece<W>(a.next, v, lw, nw);
+      if (nw.x | nw.y) store_piece<W>(a.seen, i, lw, sv | nw);
+    }
     if (a.first) {
       uint8_t* row = a.first + (size_t)i * (W * 64);
       if (nw.x) set_first_bytes(row, lw * WPL, nw.x, (uint32_t)a.rr);
@@ -278,9 +346,19 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   st.c[S_NEW_BITS] += tot;
   st.c[S_RECEIVERS] += 1;
   st.c[S_WRITTEN] += 1;
+  st.c[S_NEXT_ARCS] += (u64)(uint32_t)max(a.deg_live[v], 0);
 }
 
-// main pull kernel: one wave per vertex, a.vpw consecutive vertices per wave
+__device__ __forceinline__ u64 wave_sum_u64(u64 x) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) x += __shfl_xor(x, s);
+  return x;
+}
+
+// main pull kernel: a wave owns 64 consecutive vertices.  The per-vertex
+// checks (sender accounting, down / done / hub / no in-arcs) run lane-parallel
+// with coalesced loads; the wave then gathers, one vertex at a time, only for
+// the vertices that can still receive something.
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
@@ -290,30 +368,46 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
   const int g = lane / LPR, lw = lane % LPR;
   WaveStats st;
   ws_zero(st);
-  const int64_t first_i = ((int64_t)blockIdx.x * WAVES + wib) * a.vpw;
-  const int64_t last_i = min(first_i + a.vpw, a.nloc);
-  for (int64_t i = first_i; i < last_i; ++i) {
-    const int v = (int)(a.vbegin + i);
-    const uint32_t fp = a.fpop[v];
-    if (fp) {
-      st.c[S_SENDS] += (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
-      st.c[S_ACTIVE] += 1;
+  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
+  if (base < a.nloc) {
+    const int64_t li = base + lane;
+    bool need = false, act = false;
+    u64 sends = 0;
+    int64_t b = 0, e = 0;
+    if (li < a.nloc) {
+      const int v = (int)(a.vbegin + li);
+      const uint32_t fp = a.fpop[v];
+      act = fp != 0u;
+      if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
+      b = a.row_ptr[v];
+      e = a.row_ptr[v + 1];
+      const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
+      need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
+      if (!need && !hub) a.fpop_next[v] = 0;
     }
-    if (a.state[v] & ST_DOWN) {
-      if (lane == 0) a.fpop_next[v] = 0;
-      continue;
+    st.c[S_SENDS] += wave_sum_u64(sends);
+    st.c[S_ACTIVE] += (u64)__popcll(__ballot(act));
+    u64 m = __ballot(need);
+    while (m) {
+      const int k = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int64_t i = base + k;
+      const int v = (int)(a.vbegin + i);
+      const int64_t vb = __shfl(b, k), ve = __shfl(e, k);
+      st.c[S_VISITED] += 1;
+      const bool ee = a.early_exit != 0;
+      u64x2 acc = {0, 0}, sv = {0, 0}, cm = {0, 0};
+      if (ee) {
+        st.c[S_SEEN_READ] += 1;
+        if (g == 0) {
+          sv = a.steer ? load_piece_nt<W>(a.seen, i, lw) : load_piece<W>(a.seen, i, lw);
+          cm = load_piece<W>(a.cmask, a.midx[v], lw);
+        }
+      }
+      gather<W>(a, vb, ve, s_idx[wib], lane, g, lw, acc, st, ee, sv, cm);
+      reduce_slots<W>(acc);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, ee, sv);
     }
-    if (a.seenpop[i] >= (uint32_t)a.m_total) {
-      if (lane == 0) a.fpop_next[v] = 0;
-      continue;
-    }
-    const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
-    if (e - b > a.hub_thr) continue;   // split over waves by the hub kernels
-    st.c[S_VISITED] += 1;
-    u64x2 acc = {0, 0};
-    gather<W>(a, b, e, s_idx[wib], lane, g, lw, acc, st);
-    reduce_slots<W>(acc);
-    finish_row<W>(a, v, i, acc, lane, g, lw, st);
   }
   flush_stats(st, a.partial);
 }
@@ -333,8 +427,14 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
     const HubItem h = a.hub_items[it];
     const int64_t i = h.v - a.vbegin;
     u64x2 acc = {0, 0};
-    if (!(a.state[h.v] & ST_DOWN) && a.seenpop[i] < (uint32_t)a.m_total) {
-      gather<W>(a, h.beg, h.end, s_idx[wib], lane, g, lw, acc, st);
+    if (!(a.state[h.v] & ST_DOWN) && a.seenpop[i] < a.done_at[h.v]) {
+      const bool ee = a.early_exit != 0;
+      u64x2 sv = {0, 0}, cm = {0, 0};
+      if (ee && g == 0) {
+        sv = load_piece<W>(a.seen, i, lw);
+        cm = load_piece<W>(a.cmask, a.midx[h.v], lw);
+      }
+      gather<W>(a, h.beg, h.end, s_idx[wib], lane, g, lw, acc, st, ee, sv, cm);
       reduce_slots<W>(acc);
     }
     const bool nz = __any((acc.x | acc.y) != 0);
@@ -357,7 +457,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
   if (h < a.n_items) {
     const int v = a.hubs[h];
     const int64_t i = v - a.vbegin;
-    if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= (uint32_t)a.m_total) {
+    if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= a.done_at[v]) {
       if (lane == 0) a.fpop_next[v] = 0;
     } else {
       st.c[S_VISITED] += 1;
@@ -371,6 +471,258 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
     }
   }
   flush_stats(st, a.partial);
+}
+
+// ---------------------------------------------------------------------------
+// push mode for sparse rounds (direction-optimising, Beamer et al. SC'12):
+// every active sender ORs the NON-ZERO words of its frontier row into the
+// accumulator rows of its live out-neighbours (64-bit atomicOr, order-free so
+// bit-exact), the first push into a receiver appends it to `touched`; k_apply
+// then runs the same receiver side as the pull (finish_row) and re-zeroes acc.
+
+// active senders from the bitmap: one thread per 64-vertex word, block-level
+// compaction, one cursor add per block; big senders go to their own list
+__global__ __launch_bounds__(BLOCK) void k_active_list(const u64* __restrict__ abits, int64_t nwords,
+                                                       const int64_t* __restrict__ orp, int32_t big_thr,
+                                                       int32_t* __restrict__ active, int32_t* __restrict__ big,
+                                                       u64* __restrict__ stats) {
+  __shared__ uint32_t s_cnt[BLOCK];
+  __shared__ u64 s_base;
+  const int64_t w = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const u64 bits = w < nwords ? abits[w] : 0ull;
+  s_cnt[threadIdx.x] = (uint32_t)__popcll(bits);
+  __syncthreads();
+  for (int o = 1; o < BLOCK; o <<= 1) {   // inclusive scan
+    const uint32_t x = threadIdx.x >= o ? s_cnt[threadIdx.x - o] : 0u;
+    __syncthreads();
+    s_cnt[threadIdx.x] += x;
+    __syncthreads();
+  }
+  if (threadIdx.x == BLOCK - 1) s_base = atomicAdd(&stats[S_ACTIVE_CURSOR], (u64)s_cnt[BLOCK - 1]);
+  __syncthreads();
+  u64 pos = s_base + s_cnt[threadIdx.x] - (uint32_t)__popcll(bits);
+  u64 m = bits;
+  while (m) {
+    const int b = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const int32_t u = (int32_t)(w * 64 + b);
+    if (orp[u + 1] - orp[u] > big_thr) {
+      const u64 k = atomicAdd(&stats[S_BIG_CURSOR], 1ull);
+      big[k] = u;
+      active[pos++] = -1;   // placeholder keeps the block's slots dense
+    } else {
+      active[pos++] = u;
+    }
+  }
+}
+
+// push arcs [jb, je) of sender u; the wave holds u's row and its non-zero
+// word indices in LDS
+template <int W>
+__device__ __forceinline__ void push_arcs(const ExpandArgs& a, int64_t jb, int64_t je,
+                                          const u64* __restrict__ srow, const int8_t* __restrict__ swords,
+                                          int nnz, int lane) {
+  const int64_t T = (je - jb) * nnz;
+  for (int64_t t0 = 0; t0 < T; t0 += 64) {
+    const int64_t t = t0 + lane;
+    bool app = false;
+    int32_t v = -1;
+    if (t < T) {
+      const int64_t j = t / nnz;
+      const int q = (int)(t - j * nnz);
+      v = a.ocol[jb + j];
+      if (v >= a.vbegin && v < a.vbegin + a.nloc && !(a.state[v] & ST_DOWN) &&
+          a.seenpop[v - a.vbegin] < a.done_at[v]) {
+        const int w = swords[q];
+        atomicOr(&a.acc[(size_t)v * W + w], srow[w]);
+        if (q == 0) app = atomicExch(&a.touch[v], a.rr - 1) != a.rr - 1;
+      }
+    }
+    const u64 m = __ballot(app);
+    if (m) {
+      u64 base = 0;
+      if (lane == 0) base = atomicAdd(&a.stats[S_TOUCH_CURSOR], (u64)__popcll(m));
+      base = __shfl(base, 0);
+      if (app) a.touched[base + (u64)lane_rank(m)] = v;
+    }
+  }
+}
+
+template <int W>
+__device__ __forceinline__ int stage_row(const ExpandArgs& a, int32_t u, u64* __restrict__ srow,
+                                         int8_t* __restrict__ swords, int lane) {
+  u64 x = 0;
+  if (lane < W) x = a.front[(size_t)u * W + lane];
+  const u64 nzm = __ballot(x != 0ull);
+  if (lane < W) srow[lane] = x;
+  if (x) swords[lane_rank(nzm)] = (int8_t)lane;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return __popcll(nzm);
+}
+
+__device__ __forceinline__ void push_sender_stats(const ExpandArgs& a, int32_t u, WaveStats& st) {
+  if (u >= a.vbegin && u < a.vbegin + a.nloc) {
+    st.c[S_SENDS] += (u64)a.fpop[u] * (u64)(uint32_t)max(a.deg_live[u], 0);
+    st.c[S_ACTIVE] += 1;
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_push(ExpandArgs a) {
+  __shared__ u64 s_row[WAVES][64];
+  __shared__ int8_t s_words[WAVES][64];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  WaveStats st;
+  ws_zero(st);
+  const int64_t nact = (int64_t)a.stats[S_ACTIVE_CURSOR];
+  const int64_t stride = (int64_t)gridDim.x * WAVES;
+  for (int64_t k = (int64_t)blockIdx.x * WAVES + wib; k < nact; k += stride) {
+    const int32_t u = a.active[k];
+    if (u < 0) continue;   // big sender, pushed by k_push_big
+    push_sender_stats(a, u, st);
+    const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
+    const int64_t jb = a.orp[u], je = a.orp[u + 1];
+    st.c[S_GATHERED] += 1;
+    st.c[S_ARCS] += (u64)(je - jb);
+    st.c[S_ATOMICS] += (u64)(je - jb) * (u64)nnz;
+    push_arcs<W>(a, jb, je, s_row[wib], s_words[wib], nnz, lane);
+    __builtin_amdgcn_wave_barrier();
+  }
+  flush_stats(st, a.partial);
+}
+
+// big senders (out-degree > PUSH_CHUNK): chunk c of big sender k goes to wave
+// (k * 7919 + c) mod #waves, which spreads every sender's chunks (and the
+// senders) evenly over the grid without a prefix sum
+constexpr int PUSH_CHUNK = 512;
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_push_big(ExpandArgs a) {
+  __shared__ u64 s_row[WAVES][64];
+  __shared__ int8_t s_words[WAVES][64];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  WaveStats st;
+  ws_zero(st);
+  const int64_t nbig = (int64_t)a.stats[S_BIG_CURSOR];
+  const int64_t gw = (int64_t)blockIdx.x * WAVES + wib, nw = (int64_t)gridDim.x * WAVES;
+  for (int64_t k = 0; k < nbig; ++k) {
+    const int32_t u = a.big[k];
+    const int64_t jb = a.orp[u], je = a.orp[u + 1];
+    const int64_t nch = (je - jb + PUSH_CHUNK - 1) / PUSH_CHUNK;
+    const int64_t c0 = ((gw - (k * 7919) % nw) % nw + nw) % nw;   // first chunk of this wave
+    if (c0 == 0 && gw == (k * 7919) % nw) {
+      push_sender_stats(a, u, st);
+      st.c[S_GATHERED] += 1;
+    }
+    if (c0 >= nch) continue;
+    const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
+    for (int64_t c = c0; c < nch; c += nw) {
+      const int64_t cb = jb + c * PUSH_CHUNK, ce = min(je, cb + PUSH_CHUNK);
+      st.c[S_ARCS] += (u64)(ce - cb);
+      st.c[S_ATOMICS] += (u64)(ce - cb) * (u64)nnz;
+      push_arcs<W>(a, cb, ce, s_row[wib], s_words[wib], nnz, lane);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  flush_stats(st, a.partial);
+}
+
+// receiver side of the push: one wave per touched vertex
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
+  constexpr int LPR = Geo<W>::LPR;
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  WaveStats st;
+  ws_zero(st);
+  const int64_t nt = (int64_t)a.stats[S_TOUCH_CURSOR];
+  const int64_t stride = (int64_t)gridDim.x * WAVES;
+  for (int64_t k = (int64_t)blockIdx.x * WAVES + wib; k < nt; k += stride) {
+    const int32_t v = a.touched[k];
+    const int64_t i = v - a.vbegin;
+    u64x2 acc = {0, 0};
+    if (g == 0) {
+      acc = load_piece<W>(a.acc, v, lw);
+      store_piece<W>(a.acc, v, lw, u64x2{0, 0});
+    }
+    st.c[S_VISITED] += 1;
+    finish_row<W>(a, v, i, acc, lane, g, lw, st);
+  }
+  flush_stats(st, a.partial);
+}
+
+// frontier activity bitmap: bit v of abits = (fpop[v] != 0); one wave per 64 vertices
+__global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, u64* __restrict__ abits,
+                                                  int64_t n) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
+    const int64_t v = v0 + lane;
+    const u64 m = __ballot(v < n && fpop[v] != 0u);
+    if (lane == 0) abits[v0 >> 6] = m;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weakly connected components (union-find, hook larger root under smaller,
+// so the label of a component is its smallest vertex id).  A vertex holding
+// every message injected in its component can never receive anything new:
+// done_at[v] = #messages originating in comp(v) lets E_r skip it entirely.
+__device__ __forceinline__ int32_t cc_parent(const int32_t* p, int32_t x) {
+  return __hip_atomic_load(p + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ int32_t cc_find(int32_t* __restrict__ parent, int32_t x) {
+  int32_t p = cc_parent(parent, x);
+  while (p != x) {
+    const int32_t g = cc_parent(parent, p);
+    if (g != p) __hip_atomic_store(parent + x, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = p;
+    p = g;
+  }
+  return x;
+}
+__global__ void k_cc_init(int32_t* __restrict__ parent, int64_t n) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n) parent[v] = (int32_t)v;
+}
+__global__ void k_cc_union(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                           int32_t* __restrict__ parent, int64_t n) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  for (int64_t j = rp[v]; j < rp[v + 1]; ++j) {
+    int32_t a = (int32_t)v, b = col[j];
+    while (true) {
+      a = cc_find(parent, a);
+      b = cc_find(parent, b);
+      if (a == b) break;
+      if (a < b) {
+        const int32_t t = a;
+        a = b;
+        b = t;
+      }
+      const int32_t old = atomicCAS(parent + a, a, b);
+      if (old == a) break;
+      a = old;
+    }
+  }
+}
+__global__ void k_cc_final(int32_t* __restrict__ parent, int64_t n) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n) parent[v] = cc_find(parent, (int32_t)v);
+}
+__global__ void k_count_origins(const int32_t* __restrict__ origin, const uint32_t* __restrict__ gcnt,
+                                int64_t groups, const int32_t* __restrict__ comp, uint32_t* __restrict__ cnt) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < groups) atomicAdd(cnt + comp[origin[k]], gcnt[k]);
+}
+__global__ void k_done_at(const int32_t* __restrict__ comp, const uint32_t* __restrict__ cnt,
+                          uint32_t* __restrict__ done_at, int64_t n) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n) done_at[v] = cnt[comp[v]];
 }
 
 // ---------------------------------------------------------------------------
@@ -639,6 +991,13 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.col = c->d_col;
   a.front = c->d_front[c->cur];
   a.fpop = c->d_fpop[c->cur];
+  a.abits = c->d_abits;
+  a.done_at = c->d_done_at;
+  a.gcol = c->d_gcol;
+  a.midx = c->d_midx;
+  a.cmask = c->d_cmask;
+  a.early_exit = c->early_exit_now ? 1 : 0;
+  a.steer = c->cfg.hot_degree > 0 ? 1 : 0;
   a.next = c->d_front[c->cur ^ 1];
   a.fpop_next = c->d_fpop[c->cur ^ 1];
   a.seen = c->d_seen;
@@ -659,11 +1018,34 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.rr = c->round + 1;
   a.hub_thr = c->cfg.hub_threshold;
   a.vpw = 4;
+  a.orp = c->directed ? c->d_out_row_ptr : c->d_row_ptr;
+  a.ocol = c->directed ? c->d_out_col : c->d_col;
+  a.acc = c->d_acc;
+  a.touch = c->d_touch;
+  a.touched = c->d_touched;
+  a.active = c->d_active;
+  a.big = c->d_big;
+  a.stats = c->d_stats;
+}
+
+template <int W>
+static void launch_push_w(Ctx* c, ExpandArgs a) {
+  hipStream_t s = c->stream;
+  const int64_t nwords = (c->n_alloc + 63) / 64;
+  hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_abits, nwords,
+                     a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats);
+  hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_apply<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
 }
 
 template <int W>
 static void launch_expand_w(Ctx* c, ExpandArgs a) {
-  const int64_t per_block = (int64_t)WAVES * a.vpw;
+  if (c->mode_push) {
+    launch_push_w<W>(c, a);
+    return;
+  }
+  const int64_t per_block = (int64_t)WAVES * 64;
   if (a.nloc > 0)
     hipLaunchKernelGGL(k_expand<W>, dim3(grid_for(a.nloc, per_block)), dim3(BLOCK), 0, c->stream, a);
   if (c->n_hub_items > 0) {
@@ -676,6 +1058,17 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 }
 
 static int launch_expand(Ctx* c) {
+  hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
+                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc);
+  // direction: push when the senders' arcs are a small share of all arcs
+  const int r = c->round;
+  // early exit pays once frontier rows are dense: >= m/16 new bits per vertex last round
+  c->early_exit_now = c->cfg.early_exit != 0 && (double)c->prev_new_bits * 16.0 >= (double)c->n * (double)c->m;
+  const u64 inj = (size_t)r < c->inj_arcs.size() ? (u64)c->inj_arcs[(size_t)r] : 0ull;
+  const double est = (double)((r == 0 ? 0ull : c->prev_next_arcs) + inj);
+  c->mode_push = c->cfg.push_ratio > 0.0 && est * c->cfg.push_ratio <= (double)c->nnz;
+  if (c->mode_push && c->nloc() > 0)
+    GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1] + c->vbegin, 0, (size_t)c->nloc() * 4, c->stream));
   ExpandArgs a{};
   fill_expand(c, a);
   switch (c->words) {
@@ -768,7 +1161,9 @@ static void free_state(Ctx* c) {
   }
   dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_done_at);
+  dfree(&c->d_acc); dfree(&c->d_touch); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
+  dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
   c->inject.clear();
@@ -780,6 +1175,16 @@ int finish_graph(Ctx* c) {
   const int64_t* rp = c->directed ? c->d_out_row_ptr : c->d_row_ptr;
   hipLaunchKernelGGL(k_degree, dim3(grid_for(c->n, 256)), dim3(256), 0, c->stream, rp, c->d_deg_out, c->n);
   GP_HIP(hipGetLastError());
+  // weakly connected components (arcs in either direction)
+  GP_TRY(dalloc(&c->d_comp, (size_t)c->n));
+  hipLaunchKernelGGL(k_cc_init, dim3(grid_for(c->n, 256)), dim3(256), 0, c->stream, c->d_comp, c->n);
+  hipLaunchKernelGGL(k_cc_union, dim3(grid_for(c->n, 256)), dim3(256), 0, c->stream, c->d_row_ptr, c->d_col,
+                     c->d_comp, c->n);
+  hipLaunchKernelGGL(k_cc_final, dim3(grid_for(c->n, 256)), dim3(256), 0, c->stream, c->d_comp, c->n);
+  GP_HIP(hipGetLastError());
+  GP_TRY(build_gather_order(c));
+  c->h_deg_out.resize((size_t)c->n);
+  GP_HIP(hipMemcpyAsync(c->h_deg_out.data(), c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToHost, c->stream));
   c->h_row_ptr.resize((size_t)c->n + 1);
   GP_HIP(hipMemcpyAsync(c->h_row_ptr.data(), c->d_row_ptr, ((size_t)c->n + 1) * sizeof(int64_t),
                         hipMemcpyDeviceToHost, c->stream));
@@ -807,6 +1212,15 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_miss, na));
   GP_TRY(dalloc(&c->d_deg_live, na));
   GP_TRY(dalloc(&c->d_cand, na));
+  GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
+  GP_TRY(dalloc(&c->d_done_at, na));
+  c->done_at_valid = false;
+  GP_TRY(dalloc(&c->d_acc, na * W));
+  GP_HIP(hipMemset(c->d_acc, 0, na * W * 8));
+  GP_TRY(dalloc(&c->d_touch, na));
+  GP_TRY(dalloc(&c->d_touched, na));
+  GP_TRY(dalloc(&c->d_active, na));
+  GP_TRY(dalloc(&c->d_big, na));
   GP_TRY(dalloc(&c->d_msg_cov, W * 64 * 4));   // [local cov | local fwd | global cov | global fwd]
   c->d_msg_fwd = c->d_msg_cov + W * 64;
   c->report_cap = std::max<int64_t>(c->cfg.report_capacity, 1);
@@ -816,6 +1230,58 @@ static int alloc_state(Ctx* c) {
 }
 
 static bool state_ready(const Ctx* c) { return c->d_seen != nullptr && c->d_front[0] != nullptr; }
+
+__global__ void k_midx(const int32_t* __restrict__ comp, const int32_t* __restrict__ idx_of_root,
+                       int32_t* __restrict__ midx, int64_t n) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < n) midx[v] = idx_of_root[comp[v]];
+}
+
+// done_at[v] = number of messages originating in v's weakly connected component;
+// cmask[midx[v]] = those messages as a W-word row (the early-exit target)
+static int compute_done_at(Ctx* c, int64_t groups) {
+  uint32_t* cnt = nullptr;
+  GP_TRY(dalloc(&cnt, (size_t)c->n));
+  hipStream_t s = c->stream;
+  GP_HIP(hipMemsetAsync(cnt, 0, (size_t)c->n * 4, s));
+  GP_HIP(hipMemsetAsync(c->d_done_at, 0, (size_t)c->n_alloc * 4, s));
+  if (groups > 0)
+    hipLaunchKernelGGL(k_count_origins, dim3(grid_for(groups, 256)), dim3(256), 0, s, c->d_inj_origin,
+                       c->d_inj_cnt, groups, c->d_comp, cnt);
+  hipLaunchKernelGGL(k_done_at, dim3(grid_for(c->n, 256)), dim3(256), 0, s, c->d_comp, cnt, c->d_done_at, c->n);
+  GP_HIP(hipGetLastError());
+  GP_HIP(hipStreamSynchronize(s));
+  dfree(&cnt);
+  // component message masks (host: K <= #groups components carry messages)
+  std::vector<int32_t> comp((size_t)c->n);
+  GP_HIP(hipMemcpy(comp.data(), c->d_comp, (size_t)c->n * 4, hipMemcpyDeviceToHost));
+  std::vector<int32_t> idx_of_root((size_t)c->n, -1);
+  std::vector<u64> masks;
+  const size_t W = (size_t)c->words;
+  int32_t K = 0;
+  for (int64_t g = 0; g < groups; ++g) {
+    const int32_t root = comp[(size_t)c->h_inj_origin[(size_t)g]];
+    if (idx_of_root[(size_t)root] < 0) {
+      idx_of_root[(size_t)root] = K++;
+      masks.resize((size_t)K * W, 0);
+    }
+    u64* row = masks.data() + (size_t)idx_of_root[(size_t)root] * W;
+    for (size_t w = 0; w < W; ++w) row[w] |= c->h_inj_bits[(size_t)g * W + w];
+  }
+  if (masks.empty()) masks.assign(W, 0);
+  GP_TRY(dalloc(&c->d_cmask, masks.size()));
+  GP_HIP(hipMemcpy(c->d_cmask, masks.data(), masks.size() * 8, hipMemcpyHostToDevice));
+  int32_t* ior = nullptr;
+  GP_TRY(dalloc(&ior, (size_t)c->n));
+  GP_HIP(hipMemcpy(ior, idx_of_root.data(), (size_t)c->n * 4, hipMemcpyHostToDevice));
+  GP_TRY(dalloc(&c->d_midx, (size_t)c->n_alloc));
+  GP_HIP(hipMemset(c->d_midx, 0xFF, (size_t)c->n_alloc * 4));
+  hipLaunchKernelGGL(k_midx, dim3(grid_for(c->n, 256)), dim3(256), 0, s, c->d_comp, ior, c->d_midx, c->n);
+  GP_HIP(hipGetLastError());
+  GP_HIP(hipStreamSynchronize(s));
+  dfree(&ior);
+  return 0;
+}
 
 }  // namespace gp
 
@@ -851,6 +1317,9 @@ void gp_default_config(gp_config* cfg) {
   cfg->miss_threshold = 3;     // 2 missed heartbeats + 1 unanswered PING (Peer.py:299-311)
   cfg->hub_threshold = 4096;
   cfg->report_capacity = 1 << 20;
+  cfg->push_ratio = 40.0;   // push when sender arcs <= nnz / 40
+  cfg->early_exit = 1;
+  cfg->hot_degree = 0;
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -886,7 +1355,10 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_done_at);
+  dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
+  dfree(&c->d_acc); dfree(&c->d_touch); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
+  dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
   for (int k = 0; k < 2; ++k) { dfree(&c->d_front[k]); dfree(&c->d_fpop[k]); }
   dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
@@ -907,8 +1379,10 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
   GP_HIP(hipSetDevice(c->device));
   const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
+  const bool hot_changed = cfg->hot_degree != c->cfg.hot_degree;
   c->cfg = *cfg;
   if (c->n > 0 && hub_changed) GP_TRY(build_hubs(c));
+  if (c->n > 0 && hot_changed) GP_TRY(build_gather_order(c));
   if (state_ready(c)) GP_TRY(alloc_state(c));
   return 0;
 }
@@ -1049,6 +1523,10 @@ int gp_set_messages(gp_ctx* c, int32_t m, const int32_t* origin, const int32_t* 
     g_cnt.push_back(cnt);
     span.cnt++;
   }
+  c->inj_arcs.assign((size_t)std::max(last + 1, 0), 0);
+  for (auto& kv : c->inject)
+    for (int64_t g = kv.second.off; g < kv.second.off + kv.second.cnt; ++g)
+      c->inj_arcs[(size_t)kv.first] += c->h_deg_out[(size_t)g_origin[(size_t)g]];
   c->m = m;
   c->last_inject_round = last;
   const bool realloc = words != c->words;
@@ -1060,6 +1538,10 @@ int gp_set_messages(gp_ctx* c, int32_t m, const int32_t* origin, const int32_t* 
   GP_HIP(hipMemcpy(c->d_inj_bits, g_bits.data(), g_bits.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
   GP_HIP(hipMemcpy(c->d_inj_cnt, g_cnt.data(), g_cnt.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   if (realloc || !state_ready(c)) GP_TRY(alloc_state(c));
+  c->n_groups = (int64_t)g_origin.size();
+  c->h_inj_origin = g_origin;
+  c->h_inj_bits = g_bits;
+  c->done_at_valid = false;
   return 0;
 }
 
@@ -1067,6 +1549,10 @@ int gp_reset(gp_ctx* c) {
   if (!c) return set_error(GP_EINVAL, "null ctx");
   if (!state_ready(c)) GP_TRY(alloc_state(c));
   GP_HIP(hipSetDevice(c->device));
+  if (!c->done_at_valid) {
+    GP_TRY(compute_done_at(c, c->n_groups));
+    c->done_at_valid = true;
+  }
   const size_t W = (size_t)c->words, na = (size_t)c->n_alloc, nl = (size_t)std::max<int64_t>(c->nloc(), 1);
   hipStream_t s = c->stream;
   GP_HIP(hipMemsetAsync(c->d_seen, 0, nl * W * 8, s));
@@ -1076,6 +1562,9 @@ int gp_reset(gp_ctx* c) {
   if (c->d_first) GP_HIP(hipMemsetAsync(c->d_first, 0xFF, nl * W * 64, s));
   GP_HIP(hipMemsetAsync(c->d_digest, 0, nl * 8, s));
   GP_HIP(hipMemsetAsync(c->d_state, 0, na, s));
+  GP_HIP(hipMemsetAsync(c->d_touch, 0xFF, na * 4, s));
+  c->prev_next_arcs = 0;
+  c->prev_new_bits = 0;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
   GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToDevice, s));
@@ -1192,7 +1681,7 @@ static int round_launch(Ctx* c) {
 
   GP_HIP(hipEventRecord(c->ev[1], s));
   GP_TRY(launch_expand(c));
-  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(BLOCK), 0, s, partial, stats);
+  hipLaunchKernelGGL(k_stats_reduce, dim3(NST), dim3(BLOCK), 0, s, partial, stats);
   GP_HIP(hipGetLastError());
   GP_HIP(hipEventRecord(c->ev[2], s));
 
@@ -1241,6 +1730,9 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->seen_rows_read = h[S_SEEN_READ];
     out->rows_written = h[S_WRITTEN];
     out->vertices_visited = h[S_VISITED];
+    out->atomics = h[S_ATOMICS];
+    out->next_arcs = h[S_NEXT_ARCS];
+    out->mode = c->mode_push ? 1 : 0;
     out->overflow = (int64_t)h[S_REPORT_CURSOR] > c->report_cap ? 1 : 0;
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
@@ -1251,6 +1743,8 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->round_ms = ms;
   }
   c->last_reports = (int64_t)h[S_REPORT_CURSOR];
+  c->prev_next_arcs = h[S_NEXT_ARCS];
+  c->prev_new_bits = h[S_NEW_BITS];
   c->cur ^= 1;
   c->round = r + 1;
   return 0;
@@ -1312,9 +1806,14 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     sum.dup_reports += st.dup_reports; sum.arcs_scanned += st.arcs_scanned;
     sum.rows_gathered += st.rows_gathered; sum.seen_rows_read += st.seen_rows_read;
     sum.rows_written += st.rows_written; sum.vertices_visited += st.vertices_visited;
+    sum.atomics += st.atomics; sum.next_arcs += st.next_arcs; sum.mode = st.mode;
     sum.expand_ms = std::max(sum.expand_ms, st.expand_ms);
     sum.exchange_ms = std::max(sum.exchange_ms, st.exchange_ms);
     sum.round_ms = std::max(sum.round_ms, st.round_ms);
+  }
+  for (int32_t k = 0; k < nctx; ++k) {   // every context takes the same decisions next round
+    ctxs[k]->prev_next_arcs = sum.next_arcs;
+    ctxs[k]->prev_new_bits = sum.new_bits;
   }
   if (out) *out = sum;
   return 0;

@@ -17,10 +17,13 @@ namespace gp {
 typedef unsigned long long u64;
 
 // stats slots in the device counter block (u64 each)
+// slots [0, NST) are per-block partial sums (all-reduced across ranks);
+// the cursors above are rank-local device counters
 enum StatSlot {
   S_INJECTED = 0, S_LOST, S_NEW_BITS, S_RECEIVERS, S_SENDS, S_ACTIVE, S_CRASHED,
   S_REPORTS, S_REMOVALS, S_DUP, S_ARCS, S_GATHERED, S_SEEN_READ, S_WRITTEN,
-  S_VISITED, S_REPORT_CURSOR, S_CAND, NSTAT = 24
+  S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_RESERVED, NST,
+  S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR
 };
 
 struct HubItem {       // one wave's share of a hub's in-list
@@ -45,6 +48,7 @@ struct Ctx {
   int64_t* d_out_row_ptr = nullptr;   // directed only
   int32_t* d_out_col = nullptr;
   int32_t* d_deg_out = nullptr;
+  int32_t* d_comp = nullptr;          // weakly connected component label (min vertex id)
   std::vector<int64_t> h_row_ptr;     // host copy (hub table, partition)
 
   // partition
@@ -57,6 +61,8 @@ struct Ctx {
   int32_t m = 0, words = 0;
   std::map<int32_t, InjectSpan> inject;   // round -> groups
   int32_t last_inject_round = -1;
+  int64_t n_groups = 0;               // (round, origin) injection groups
+  bool done_at_valid = false;
   int32_t* d_inj_origin = nullptr;
   u64* d_inj_bits = nullptr;
   uint32_t* d_inj_cnt = nullptr;
@@ -73,6 +79,25 @@ struct Ctx {
   uint8_t* d_miss = nullptr;        // [n_alloc]
   int32_t* d_deg_live = nullptr;    // [n_alloc]
   int32_t* d_cand = nullptr;        // [n] detection candidates of a round
+  u64* d_abits = nullptr;           // [n_alloc/64] frontier activity bitmap
+  // push (sparse-round) mode
+  u64* d_acc = nullptr;             // [n_alloc][W] OR accumulator, kept all-zero between uses
+  int32_t* d_touch = nullptr;       // [n_alloc] round of the last push into v
+  int32_t* d_touched = nullptr;     // [n_alloc] receivers touched this round
+  int32_t* d_active = nullptr;      // [n_alloc] senders (deg <= hub threshold)
+  int32_t* d_big = nullptr;         // [n_alloc] senders above the hub threshold
+  std::vector<int64_t> inj_arcs;    // per inject round: sum of origin out-degrees
+  u64 prev_next_arcs = 0;           // out-degree sum of the last round's receivers
+  bool mode_push = false;           // direction of the current round
+  bool early_exit_now = false;      // coverage-checked scan this round
+  u64 prev_new_bits = 0;            // new bits of the last round (global)
+  int32_t* d_gcol = nullptr;        // [nnz] in-CSR columns, rows sorted by neighbour degree desc
+  int32_t* d_midx = nullptr;        // [n_alloc] component mask row of v (-1: none)
+  u64* d_cmask = nullptr;           // [K][W] messages per component
+  std::vector<int32_t> h_inj_origin;   // host copies of the injection groups
+  std::vector<u64> h_inj_bits;
+  std::vector<int32_t> h_deg_out;
+  uint32_t* d_done_at = nullptr;    // [n_alloc] messages of the vertex's component
   u64* d_msg_cov = nullptr;    // [W*64]
   u64* d_msg_fwd = nullptr;    // [W*64]
   gp_report* d_reports = nullptr;
@@ -139,6 +164,7 @@ void dfree(T** p) {
 
 // graph_build.hip
 int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed);
+int build_gather_order(Ctx* c);
 // gossip_engine.hip
 int finish_graph(Ctx* c);
 

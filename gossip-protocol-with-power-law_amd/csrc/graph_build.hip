@@ -199,4 +199,43 @@ int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed) 
   return 0;
 }
 
+// gather order: each in-list re-sorted by the neighbour's in-degree, largest
+// first (stable: ties keep ascending ids).  Hubs hold most messages earliest,
+// so the early-exit pull covers a vertex's missing set after fewer rows.
+// bit 31 of a gather-order column tags a hub row (in-degree >= hot): the pull
+// loads it with the default (cacheable) policy and everything else non-temporal
+__global__ void k_gorder_keys(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                              u64* __restrict__ keys, int32_t* __restrict__ vals, int64_t n, int64_t hot) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  for (int64_t j = rp[v]; j < rp[v + 1]; ++j) {
+    const int32_t u = col[j];
+    const uint32_t d = (uint32_t)(rp[u + 1] - rp[u]);
+    keys[j] = ((u64)v << 32) | (u64)(0xFFFFFFFFu - d);
+    vals[j] = (hot > 0 && (int64_t)d >= hot) ? (int32_t)((uint32_t)u | 0x80000000u) : u;
+  }
+}
+
+int build_gather_order(Ctx* c) {
+  hipStream_t s = c->stream;
+  const int64_t A = c->nnz;
+  GP_TRY(dalloc(&c->d_gcol, (size_t)std::max<int64_t>(A, 1)));
+  if (A == 0) return 0;
+  DevBuf ka, kb, va, tmp;
+  GP_HIP(hipMalloc(&ka.p, (size_t)A * 8));
+  GP_HIP(hipMalloc(&kb.p, (size_t)A * 8));
+  GP_HIP(hipMalloc(&va.p, (size_t)A * 4));
+  hipLaunchKernelGGL(k_gorder_keys, dim3((unsigned)((c->n + 255) / 256)), dim3(256), 0, s, c->d_row_ptr,
+                     c->d_col, (u64*)ka.p, (int32_t*)va.p, c->n, (int64_t)c->cfg.hot_degree);
+  GP_HIP(hipGetLastError());
+  size_t tb = 0;
+  GP_HIP(rocprim::radix_sort_pairs(nullptr, tb, (u64*)ka.p, (u64*)kb.p, (int32_t*)va.p, c->d_gcol, (size_t)A,
+                                   0, 64, s));
+  GP_HIP(hipMalloc(&tmp.p, std::max<size_t>(tb, 16)));
+  GP_HIP(rocprim::radix_sort_pairs(tmp.p, tb, (u64*)ka.p, (u64*)kb.p, (int32_t*)va.p, c->d_gcol, (size_t)A,
+                                   0, 64, s));
+  GP_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
 }  // namespace gp

@@ -69,6 +69,10 @@ typedef struct gp_round_stats {
   uint64_t seen_rows_read;  /* receiver seen rows read (8*W bytes each)              */
   uint64_t rows_written;    /* next rows written (+ seen rows re-written)            */
   uint64_t vertices_visited;/* receivers whose in-list was scanned                   */
+  uint64_t atomics;         /* push mode: 64-bit atomicOr issued                      */
+  uint64_t next_arcs;       /* out-degree sum of this round's receivers (direction)   */
+  int32_t mode;             /* 0 = pull expansion, 1 = push expansion                 */
+  int32_t pad;
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
@@ -91,6 +95,11 @@ typedef struct gp_config {
   int32_t miss_threshold;      /* heartbeat misses before report (reference: 3)        */
   int32_t hub_threshold;       /* in-degree above which a vertex is split over waves   */
   int64_t report_capacity;     /* reports kept per round (counts stay exact)           */
+  double push_ratio;           /* push a round when its sender arcs * push_ratio <= nnz;
+                                  0 = always pull                      */
+  int32_t early_exit;          /* coverage-checked pull scans in dense rounds (§3.4)   */
+  int32_t hot_degree;          /* > 0: rows of vertices with in-degree >= hot_degree are
+                                  loaded cacheable, all other streams non-temporal (§3.5) */
 } gp_config;
 
 /* what for gp_read */

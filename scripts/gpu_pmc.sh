@@ -1,0 +1,12 @@
+# HBM traffic of the expansion kernels: separate rocprofv3 --pmc passes
+# (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950; MI355X_MICROARCH.md)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/pmc
+export TMPDIR=/tmp
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline --profile-steps"
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc/fetch -o fetch -- python3 bench.py $ARGS > gpurun_out/pmc/fetch.json 2> gpurun_out/pmc/fetch.err
+echo "fetch exit $?"
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc/write -o write -- python3 bench.py $ARGS > gpurun_out/pmc/write.json 2> gpurun_out/pmc/write.err
+echo "write exit $?"
+find gpurun_out/pmc -name "*.csv" | head

@@ -26,11 +26,16 @@ def _engine(pkg, g, origin, inject=None, **cfg):
     return eng
 
 
-def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096, **kw):
+# expansion direction: 0 = always pull, 1e-12 = always push, 10 = adaptive (default)
+MODES = [0.0, 1e-12, 10.0]
+
+
+def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096,
+             push_ratio=10.0, **kw):
     churn = kw.get("churn", False)
     cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(bool(churn or crashes)),
                churn=int(churn), p_fail=kw.get("p_fail", 0.0), churn_seed=kw.get("churn_seed", 0),
-               hub_threshold=hub_threshold)
+               hub_threshold=hub_threshold, push_ratio=push_ratio)
     eng = _engine(pkg, g, origin, inject, **cfg)
     by_round = {}
     for v, r in crashes:
@@ -65,31 +70,39 @@ def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_th
     return out
 
 
-def test_c2_ba_10k_64(pkg, oracle):
+@pytest.mark.parametrize("push_ratio", MODES)
+def test_c2_ba_10k_64(pkg, oracle, push_ratio):
     """BASELINE config 2: 10^4-node BA(m=2), 64 concurrent messages."""
     g = pkg.overlay.barabasi_albert(10_000, 2, seed=2)
     origin = pkg.overlay.random_origins(g.n, 64, seed=2)
-    r = _compare(pkg, oracle, g, origin)
+    r = _compare(pkg, oracle, g, origin, push_ratio=push_ratio)
+    if push_ratio == 1e-12:
+        assert all(s["mode"] == 1 for s in r["stats"])
+    if push_ratio == 0.0:
+        assert all(s["mode"] == 0 for s in r["stats"])
     total = sum(s["sends"] for s in r["stats"])
     assert total == 64 * g.nnz   # connected BA: every message crosses every arc once
     r["eng"].close()
 
 
+@pytest.mark.parametrize("push_ratio", MODES)
 @pytest.mark.parametrize("m", [1, 10, 63, 64, 65, 130, 300, 1000, 4096])
-def test_message_widths(pkg, oracle, m):
+def test_message_widths(pkg, oracle, m, push_ratio):
     g = pkg.overlay.barabasi_albert(1500, 3, seed=m)
     origin = pkg.overlay.random_origins(g.n, m, seed=m)
     inject = (np.arange(m) % 5).astype(np.int32)
-    _compare(pkg, oracle, g, origin, inject)["eng"].close()
+    _compare(pkg, oracle, g, origin, inject, push_ratio=push_ratio)["eng"].close()
 
 
-def test_hub_split(pkg, oracle):
-    """Force the multi-wave hub path (partials + final) on every vertex above 64 arcs."""
+@pytest.mark.parametrize("push_ratio", MODES)
+def test_hub_split(pkg, oracle, push_ratio):
+    """Force the multi-wave hub paths (pull: partials + final; push: grid-wide
+    sweep of big senders) on every vertex above 64 arcs."""
     rp, col = oracle.chung_lu(20_000, 8, 2.2, 11)
     g = pkg.CSR(20_000, rp, col, False)
     assert np.diff(rp).max() > 1000
     origin = pkg.overlay.random_origins(g.n, 256, seed=11)
-    _compare(pkg, oracle, g, origin, hub_threshold=64)["eng"].close()
+    _compare(pkg, oracle, g, origin, hub_threshold=64, push_ratio=push_ratio)["eng"].close()
 
 
 def test_c1_directed_schedule_and_direct_deliveries(pkg, oracle):
@@ -107,20 +120,23 @@ def test_c1_directed_schedule_and_direct_deliveries(pkg, oracle):
     r["eng"].close()
 
 
-def test_churn_random(pkg, oracle):
+@pytest.mark.parametrize("push_ratio", MODES)
+def test_churn_random(pkg, oracle, push_ratio):
     g = pkg.overlay.barabasi_albert(5000, 2, seed=5)
     origin = pkg.overlay.random_origins(g.n, 128, seed=5)
     inject = (np.arange(128) % 9).astype(np.int32)
-    r = _compare(pkg, oracle, g, origin, inject, churn=True, p_fail=0.03, churn_seed=77)
+    r = _compare(pkg, oracle, g, origin, inject, churn=True, p_fail=0.03, churn_seed=77,
+                 push_ratio=push_ratio)
     assert sum(s["removals"] for s in r["stats"]) > 0
     r["eng"].close()
 
 
-def test_explicit_crashes_directed(pkg, oracle):
+@pytest.mark.parametrize("push_ratio", MODES)
+def test_explicit_crashes_directed(pkg, oracle, push_ratio):
     g = pkg.overlay.first3_overlay(10)
     origin, inject, _ = pkg.peer.c1_schedule(10)
     r = _compare(pkg, oracle, g, np.array(origin, np.int32), np.array(inject, np.int32),
-                 crashes=[(4, 1), (0, 6), (9, 3)])
+                 crashes=[(4, 1), (0, 6), (9, 3)], push_ratio=push_ratio)
     assert sum(s["removals"] for s in r["stats"]) >= 2
     r["eng"].close()
 
@@ -135,10 +151,11 @@ def test_chung_lu_device_builder_matches_oracle(pkg, oracle):
         assert np.array_equal(dg.col, col)
 
 
-def test_c3_chung_lu_1e6_1024(pkg, oracle):
+@pytest.mark.parametrize("push_ratio", MODES)
+def test_c3_chung_lu_1e6_1024(pkg, oracle, push_ratio):
     """BASELINE config 3: 10^6-node Chung-Lu (gamma 2.5), 1024 messages."""
     n = 1_000_000
-    with pkg.GossipEngine(0, track_digest=1) as eng:
+    with pkg.GossipEngine(0, track_digest=1, push_ratio=push_ratio) as eng:
         eng.build_chung_lu(n, 8, 2.5, 3)
         g = eng.graph()
         origin = pkg.overlay.random_origins(n, 1024, seed=3)
@@ -157,7 +174,8 @@ def test_c3_chung_lu_1e6_1024(pkg, oracle):
     assert np.array_equal(fwd, ref["forwards"])
 
 
-def test_group_partition_invariance(pkg, oracle):
+@pytest.mark.parametrize("push_ratio", MODES)
+def test_group_partition_invariance(pkg, oracle, push_ratio):
     """2 and 3 contexts on one GPU (device-to-device exchange) == 1 context."""
     g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
     origin = pkg.overlay.random_origins(g.n, 200, seed=8)
@@ -166,7 +184,8 @@ def test_group_partition_invariance(pkg, oracle):
     for P in (2, 3):
         engs = []
         for k in range(P):
-            e = pkg.GossipEngine(0, track_first=1, churn=1, p_fail=0.02, churn_seed=3, track_msg_forwards=1)
+            e = pkg.GossipEngine(0, track_first=1, churn=1, p_fail=0.02, churn_seed=3, track_msg_forwards=1,
+                                 push_ratio=push_ratio)
             e.load_graph(g)
             e.set_partition(k, P)
             e.set_messages(origin, inject)
@@ -192,16 +211,18 @@ def test_group_partition_invariance(pkg, oracle):
             e.close()
 
 
-def test_edge_cases(pkg, oracle):
+@pytest.mark.parametrize("push_ratio", MODES)
+def test_edge_cases(pkg, oracle, push_ratio):
     # isolated vertices, a single message, origin that crashes before injection
     g = pkg.CSR.from_edges(50, [(0, 1), (1, 2), (2, 3), (10, 11)])
-    _compare(pkg, oracle, g, np.array([0], np.int32))["eng"].close()
-    _compare(pkg, oracle, g, np.array([7, 7, 7], np.int32))["eng"].close()
+    kw = dict(push_ratio=push_ratio)
+    _compare(pkg, oracle, g, np.array([0], np.int32), **kw)["eng"].close()
+    _compare(pkg, oracle, g, np.array([7, 7, 7], np.int32), **kw)["eng"].close()
     _compare(pkg, oracle, g, np.array([0, 10, 2], np.int32), np.array([0, 2, 4], np.int32),
-             crashes=[(10, 1)])["eng"].close()
+             crashes=[(10, 1)], **kw)["eng"].close()
     # all messages at one origin of a star (hub receives nothing new after round 1)
     star = pkg.CSR.from_edges(200, [(0, i) for i in range(1, 200)])
-    _compare(pkg, oracle, star, np.full(100, 5, np.int32), hub_threshold=64)["eng"].close()
+    _compare(pkg, oracle, star, np.full(100, 5, np.int32), hub_threshold=64, **kw)["eng"].close()
 
 
 def test_full_size_invariants_c3(pkg):
