@@ -190,7 +190,7 @@ struct ExpandArgs {
   const int64_t* __restrict__ orp;     // out-CSR (undirected: == row_ptr/col)
   const int32_t* __restrict__ ocol;
   u64* __restrict__ acc;               // [n_alloc][W] OR accumulator (all-zero between uses)
-  int32_t* __restrict__ touch;         // [n_alloc] last round v was pushed to
+  u64* __restrict__ tbits;             // [n_alloc/64] receivers pushed to this round
   int32_t* __restrict__ touched;       // receivers touched this round
   const int32_t* __restrict__ active;  // senders with deg <= hub_thr
   const int32_t* __restrict__ big;     // senders with deg > hub_thr
@@ -477,8 +477,9 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
 // push mode for sparse rounds (direction-optimising, Beamer et al. SC'12):
 // every active sender ORs the NON-ZERO words of its frontier row into the
 // accumulator rows of its live out-neighbours (64-bit atomicOr, order-free so
-// bit-exact), the first push into a receiver appends it to `touched`; k_apply
-// then runs the same receiver side as the pull (finish_row) and re-zeroes acc.
+// bit-exact) and sets the receiver's bit in `tbits` (fire-and-forget atomicOr
+// on a 2 MB bitmap); k_touch_list compacts the bitmap and k_apply runs the same
+// receiver side as the pull (finish_row) and re-zeroes acc.
 
 // active senders from the bitmap: one thread per 64-vertex word, block-level
 // compaction, one cursor add per block; big senders go to their own list
@@ -525,7 +526,6 @@ __device__ __forceinline__ void push_arcs(const ExpandArgs& a, int64_t jb, int64
   const int64_t T = (je - jb) * nnz;
   for (int64_t t0 = 0; t0 < T; t0 += 64) {
     const int64_t t = t0 + lane;
-    bool app = false;
     int32_t v = -1;
     if (t < T) {
       const int64_t j = t / nnz;
@@ -535,16 +535,38 @@ __device__ __forceinline__ void push_arcs(const ExpandArgs& a, int64_t jb, int64
           a.seenpop[v - a.vbegin] < a.done_at[v]) {
         const int w = swords[q];
         atomicOr(&a.acc[(size_t)v * W + w], srow[w]);
-        if (q == 0) app = atomicExch(&a.touch[v], a.rr - 1) != a.rr - 1;
+        if (q == 0) atomicOr(&a.tbits[v >> 6], 1ull << (v & 63));
       }
     }
-    const u64 m = __ballot(app);
-    if (m) {
-      u64 base = 0;
-      if (lane == 0) base = atomicAdd(&a.stats[S_TOUCH_CURSOR], (u64)__popcll(m));
-      base = __shfl(base, 0);
-      if (app) a.touched[base + (u64)lane_rank(m)] = v;
-    }
+  }
+}
+
+// touched receivers: compact the bitmap (one thread per word) and clear it
+__global__ __launch_bounds__(BLOCK) void k_touch_list(u64* __restrict__ tbits, int64_t nwords,
+                                                      int32_t* __restrict__ touched, u64* __restrict__ stats) {
+  __shared__ uint32_t s_cnt[BLOCK];
+  __shared__ u64 s_base;
+  const int64_t w = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  u64 bits = 0;
+  if (w < nwords) {
+    bits = tbits[w];
+    if (bits) tbits[w] = 0ull;
+  }
+  s_cnt[threadIdx.x] = (uint32_t)__popcll(bits);
+  __syncthreads();
+  for (int o = 1; o < BLOCK; o <<= 1) {   // inclusive scan
+    const uint32_t x = threadIdx.x >= o ? s_cnt[threadIdx.x - o] : 0u;
+    __syncthreads();
+    s_cnt[threadIdx.x] += x;
+    __syncthreads();
+  }
+  if (threadIdx.x == BLOCK - 1) s_base = atomicAdd(&stats[S_TOUCH_CURSOR], (u64)s_cnt[BLOCK - 1]);
+  __syncthreads();
+  u64 pos = s_base + s_cnt[threadIdx.x] - (uint32_t)__popcll(bits);
+  while (bits) {
+    const int b = __ffsll((long long)bits) - 1;
+    bits &= bits - 1;
+    touched[pos++] = (int32_t)(w * 64 + b);
   }
 }
 
@@ -1021,7 +1043,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.orp = c->directed ? c->d_out_row_ptr : c->d_row_ptr;
   a.ocol = c->directed ? c->d_out_col : c->d_col;
   a.acc = c->d_acc;
-  a.touch = c->d_touch;
+  a.tbits = c->d_tbits;
   a.touched = c->d_touched;
   a.active = c->d_active;
   a.big = c->d_big;
@@ -1036,6 +1058,8 @@ static void launch_push_w(Ctx* c, ExpandArgs a) {
                      a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats);
   hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_touch_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_tbits, nwords,
+                     c->d_touched, c->d_stats);
   hipLaunchKernelGGL(k_apply<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
 }
 
@@ -1162,7 +1186,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_done_at);
-  dfree(&c->d_acc); dfree(&c->d_touch); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
+  dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -1217,7 +1241,8 @@ static int alloc_state(Ctx* c) {
   c->done_at_valid = false;
   GP_TRY(dalloc(&c->d_acc, na * W));
   GP_HIP(hipMemset(c->d_acc, 0, na * W * 8));
-  GP_TRY(dalloc(&c->d_touch, na));
+  GP_TRY(dalloc(&c->d_tbits, (na + 63) / 64));
+  GP_HIP(hipMemset(c->d_tbits, 0, (na + 63) / 64 * 8));
   GP_TRY(dalloc(&c->d_touched, na));
   GP_TRY(dalloc(&c->d_active, na));
   GP_TRY(dalloc(&c->d_big, na));
@@ -1357,7 +1382,7 @@ void gp_destroy(gp_ctx* c) {
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
   dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_done_at);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
-  dfree(&c->d_acc); dfree(&c->d_touch); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
+  dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
   for (int k = 0; k < 2; ++k) { dfree(&c->d_front[k]); dfree(&c->d_fpop[k]); }
   dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
@@ -1562,7 +1587,7 @@ int gp_reset(gp_ctx* c) {
   if (c->d_first) GP_HIP(hipMemsetAsync(c->d_first, 0xFF, nl * W * 64, s));
   GP_HIP(hipMemsetAsync(c->d_digest, 0, nl * 8, s));
   GP_HIP(hipMemsetAsync(c->d_state, 0, na, s));
-  GP_HIP(hipMemsetAsync(c->d_touch, 0xFF, na * 4, s));
+  GP_HIP(hipMemsetAsync(c->d_tbits, 0, (na + 63) / 64 * 8, s));
   c->prev_next_arcs = 0;
   c->prev_new_bits = 0;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));

@@ -82,7 +82,7 @@ struct Ctx {
   u64* d_abits = nullptr;           // [n_alloc/64] frontier activity bitmap
   // push (sparse-round) mode
   u64* d_acc = nullptr;             // [n_alloc][W] OR accumulator, kept all-zero between uses
-  int32_t* d_touch = nullptr;       // [n_alloc] round of the last push into v
+  u64* d_tbits = nullptr;           // [n_alloc/64] receivers pushed to this round
   int32_t* d_touched = nullptr;     // [n_alloc] receivers touched this round
   int32_t* d_active = nullptr;      // [n_alloc] senders (deg <= hub threshold)
   int32_t* d_big = nullptr;         // [n_alloc] senders above the hub threshold

@@ -1,8 +1,17 @@
-# parameter sweep of the C4 bench (no CPU baseline); one JSON line per setting
+# parameter sweep of the C4 bench (no CPU baseline): PARAM=<bench flag> LIST="<values>"
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/sweep
-for hd in ${HOT_LIST:-0 32 64 128 256}; do
-  timeout -k 10 120 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --hot-degree $hd --profile-steps $EXTRA > gpurun_out/sweep/hot_$hd.json 2> gpurun_out/sweep/hot_$hd.err || exit 1
-  python -c "import json,sys; d=json.loads(open('gpurun_out/sweep/hot_$hd.json').read()); print('hot', $hd, round(d['value']), 'GTEPS', round(d['ms_per_step'],2), 'ms')"
+PARAM=${PARAM:---hot-degree}
+for val in ${LIST:-0 64}; do
+  tag=$(echo "$PARAM$val" | tr -c 'a-zA-Z0-9.' '_')
+  timeout -k 10 120 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline $PARAM $val --profile-steps $EXTRA > gpurun_out/sweep/$tag.json 2> gpurun_out/sweep/$tag.err || exit 1
+  python - "$tag" "$PARAM" "$val" <<'PY'
+import json, sys
+tag, p, v = sys.argv[1:]
+d = json.loads(open(f"gpurun_out/sweep/{tag}.json").read())
+rs = [json.loads(l) for l in open(f"gpurun_out/sweep/{tag}.err") if l.startswith("{")]
+print(p, v, round(d["value"]), "GTEPS", round(d["ms_per_step"], 2), "ms |",
+      " ".join(f"r{r['round']}:{'P' if r['mode'] else 'L'}{r['expand_ms']:.2f}" for r in rs))
+PY
 done
