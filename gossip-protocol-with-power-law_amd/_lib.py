@@ -47,6 +47,8 @@ class RoundStats(ctypes.Structure):
         ("vertices_visited", ctypes.c_uint64),
         ("atomics", ctypes.c_uint64),
         ("next_arcs", ctypes.c_uint64),
+        ("sparse_gathered", ctypes.c_uint64),
+        ("sparse_written", ctypes.c_uint64),
         ("mode", ctypes.c_int32),
         ("pad", ctypes.c_int32),
         ("expand_ms", ctypes.c_double),
@@ -76,6 +78,8 @@ class Config(ctypes.Structure):
         ("push_ratio", ctypes.c_double),
         ("early_exit", ctypes.c_int32),
         ("hot_degree", ctypes.c_int32),
+        ("sparse_rows", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
     ]
 
 

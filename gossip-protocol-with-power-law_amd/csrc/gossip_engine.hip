@@ -118,25 +118,37 @@ __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirs
 
 // ---------------------------------------------------------------------------
 // per-wave counters, flushed once per block into one of NPART slots
+// Per-wave counters live in LDS (one row per wave, written by lane 0 only):
+// every update is wave-uniform, and keeping NST u64 counters out of the VGPR
+// file is worth several waves per SIMD of occupancy in the gather kernels.
+__device__ __forceinline__ u64* stats_lds() {
+  __shared__ u64 rows[WAVES][NST];
+  return &rows[0][0];
+}
 struct WaveStats {
-  u64 c[NST];
+  u64* row;
+  bool lead;
+  __device__ __forceinline__ void add(int k, u64 x) {
+    if (lead) row[k] += x;
+  }
 };
 __device__ __forceinline__ void ws_zero(WaveStats& s) {
-#pragma unroll
-  for (int k = 0; k < NST; ++k) s.c[k] = 0;
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  s.row = stats_lds() + wib * NST;
+  s.lead = lane == 0;
+  if (lane < NST) s.row[lane] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 __device__ void flush_stats(const WaveStats& s, u64* __restrict__ partial) {
-  __shared__ u64 red[WAVES][NST];
-  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < NST; ++k) red[wib][k] = s.c[k];
-  }
+  (void)s;
+  u64* red = stats_lds();
   __syncthreads();
   if (threadIdx.x < NST) {
     u64 t = 0;
 #pragma unroll
-    for (int w = 0; w < WAVES; ++w) t += red[w][threadIdx.x];
+    for (int w = 0; w < WAVES; ++w) t += red[w * NST + threadIdx.x];
     if (t) atomicAdd(&partial[(size_t)threadIdx.x * NPART + (blockIdx.x % NPART)], t);
   }
 }
@@ -166,6 +178,11 @@ struct ExpandArgs {
   const u64* __restrict__ front;       // frontier_r
   const uint32_t* __restrict__ fpop;   // |frontier_r|
   const u64* __restrict__ abits;       // bit v: frontier_r(v) != 0 (2 MB at 2^24: L2-resident)
+  const u64* __restrict__ sbits;       // bit v: frontier_r(v) stored as an id list
+  const uint16_t* __restrict__ ids;    // [n_alloc][SPK] id lists of frontier_r (null: dense only)
+  const uint8_t* __restrict__ fmt;     // [n_alloc] 1 = id list (valid iff fpop != 0)
+  uint16_t* __restrict__ ids_next;
+  uint8_t* __restrict__ fmt_next;
   const int32_t* __restrict__ gcol;    // in-CSR columns in gather order (neighbour degree desc)
   const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
@@ -203,6 +220,42 @@ struct ExpandArgs {
   int32_t vpw;                         // vertices per wave (k_expand)
 };
 
+// Sparse frontier rows: a row with at most SPK new bits is
+// written as a list of SPK u16 message ids (64 B, 0xFFFF = empty) instead of
+// the 8W-byte bitmap row; the gather ORs such rows into a per-wave LDS row with
+// ds_or_b64.  Only for W >= 32 (rows >= 256 B).
+constexpr int SPK = 32;
+// rows each lane keeps in flight per gather step (MLP vs VGPRs)
+#ifndef GP_ROWS_IN_FLIGHT
+#define GP_ROWS_IN_FLIGHT 4
+#endif
+constexpr uint16_t SP_EMPTY = 0xFFFF;
+
+struct WaveLds {
+  int32_t idx[64];      // dense-format active neighbours (tagged ids)
+  int32_t sidx[64];     // id-list-format active neighbours
+  u64 acc[64];          // OR accumulator of id-list rows
+  u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
+  uint16_t ids[64];     // id-list staging of finish_row
+  uint32_t nids;        // id-list fill cursor
+};
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t x, int lane) {
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  return inc - x;
+}
+
 // OR-reduce the row slots of the wave: afterwards every lane holds the full
 // result for its lw column.
 template <int W>
@@ -218,58 +271,82 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
 // OR the frontier rows of the active in-neighbours in arcs [b, e) into acc.
 // Neighbour ids come 64 at a time from the gather-order CSR (in-lists sorted
 // by neighbour degree, hubs first), are filtered by the L2-resident activity
-// bitmap and staged in LDS compacted to the active ones.
+// bitmap and staged in LDS compacted to the active ones; id-list rows are
+// folded through the LDS row first, dense rows then stream into registers.
 // Early exit (bottom-up, Beamer et al. SC'12): with `ee` the wave stops once
 // acc | seen covers every message of the vertex's component (cm) -- group-0
 // lanes hold the seen (sv) and mask (cm) pieces.  OR is idempotent, so
 // acc & ~seen is exactly what the full scan would give.
 template <int W>
-__device__ __forceinline__ void gather(const ExpandArgs& a, int64_t b, int64_t e,
-                                       int32_t* __restrict__ sidx, int lane, int g, int lw,
-                                       u64x2& acc, WaveStats& st, bool ee, u64x2 sv, u64x2 cm) {
+__device__ __forceinline__ void gather(const ExpandArgs& a, int64_t b, int64_t e, WaveLds& L,
+                                       int lane, int g, int lw, u64x2& acc, WaveStats& st, bool ee,
+                                       u64x2 want) {
   constexpr int RPI = Geo<W>::RPI;
+  constexpr int WPL = Geo<W>::WPL;
+  const bool sparse_ok = (W >= 32) && a.ids != nullptr;
   for (int64_t j0 = b; j0 < e; j0 += 64) {
     const int n = (int)min((int64_t)64, e - j0);
     int32_t tu = 0;   // column id, bit 31 = hub row (cache-steered)
-    bool act = false;
+    bool act = false, spr = false;
     if (lane < n) {
       tu = a.steer ? __builtin_nontemporal_load(a.gcol + j0 + lane) : a.gcol[j0 + lane];
       const int32_t u = tu & 0x7FFFFFFF;
       act = (a.abits[u >> 6] >> (u & 63)) & 1ull;
+      if (act && sparse_ok) spr = (a.sbits[u >> 6] >> (u & 63)) & 1ull;
     }
-    const u64 mask = __ballot(act);
-    const int cnt = __popcll(mask);
-    st.c[S_ARCS] += n;
-    if (cnt == 0) continue;
-    if (act) sidx[lane_rank(mask)] = tu;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const u64 dmask = __ballot(act && !spr);
+    const u64 smask = __ballot(spr);
+    const int cnt = __popcll(dmask), scnt = __popcll(smask);
+    st.add(S_ARCS, n);
+    if (cnt + scnt == 0) continue;
+    if (act && !spr) L.idx[lane_rank(dmask)] = tu;
+    if (spr) L.sidx[lane_rank(smask)] = tu & 0x7FFFFFFF;
+    if (scnt) {
+      if (lane < W) L.acc[lane] = 0ull;
+      wave_sync_lds();
+      for (int k0 = 0; k0 < scnt; k0 += 64 / SPK) {   // two id lists per wave-instruction
+        const int k = k0 + lane / SPK;
+        if (k < scnt) {
+          const int32_t u = L.sidx[k];
+          const uint16_t id = a.ids[(size_t)u * SPK + (lane % SPK)];
+          if (id != SP_EMPTY) atomicOr(&L.acc[id >> 6], 1ull << (id & 63));
+        }
+      }
+      wave_sync_lds();
+      if (g == 0) {
+        acc.x |= L.acc[lw * WPL];
+        if constexpr (WPL == 2) acc.y |= L.acc[lw * WPL + 1];
+      }
+      st.add(S_GATHERED, scnt);
+      st.add(S_SP_GATHERED, scnt);
+    } else {
+      wave_sync_lds();
+    }
     bool stop = false;
-    for (int k0 = 0; k0 < cnt; k0 += 4 * RPI) {
-      const int k = k0 + g, k1 = k + RPI, k2 = k + 2 * RPI, k3 = k + 3 * RPI;
+    for (int k0 = 0; k0 < cnt; k0 += GP_ROWS_IN_FLIGHT * RPI) {
       const bool steer = a.steer != 0;
-      u64x2 r0 = {0, 0}, r1 = {0, 0}, r2 = {0, 0}, r3 = {0, 0};
-      if (k < cnt) r0 = load_row<W>(a.front, sidx[k], lw, steer);
-      if (k1 < cnt) r1 = load_row<W>(a.front, sidx[k1], lw, steer);
-      if (k2 < cnt) r2 = load_row<W>(a.front, sidx[k2], lw, steer);
-      if (k3 < cnt) r3 = load_row<W>(a.front, sidx[k3], lw, steer);
-      acc |= (r0 | r1) | (r2 | r3);
-      st.c[S_GATHERED] += (u64)min(4 * RPI, cnt - k0);
+      u64x2 r[GP_ROWS_IN_FLIGHT];
+#pragma unroll
+      for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
+        const int k = k0 + g + q * RPI;
+        r[q] = u64x2{0, 0};
+        if (k < cnt) r[q] = load_row<W>(a.front, L.idx[k], lw, steer);
+      }
+#pragma unroll
+      for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
+      st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
       if (ee) {
         u64x2 t = acc;
         reduce_slots<W>(t);
         u64x2 miss = {0, 0};
-        if (g == 0) miss = cm & ~(t | sv);
+        if (g == 0) miss = want & ~t;
         if (!__any((miss.x | miss.y) != 0ull)) {
           stop = true;
           break;
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync_lds();
     if (stop) break;
   }
 }
@@ -296,18 +373,22 @@ __device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int w
 // receiver side of vertex v (local index i): apply seen, write next, counters
 template <int W>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
-                                           int g, int lw, WaveStats& st, bool have_sv = false,
-                                           u64x2 sv_pre = u64x2{0, 0}) {
+                                           int g, int lw, WaveStats& st, WaveLds& L, bool have_sv = false) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
     if (lane == 0) a.fpop_next[v] = 0;
     return;
   }
-  if (!have_sv) st.c[S_SEEN_READ] += 1;
+  if (!have_sv) st.add(S_SEEN_READ, 1);
   u64x2 sv = {0, 0}, nw = {0, 0};
   if (g == 0) {
-    sv = have_sv ? sv_pre : (a.steer ? load_piece_nt<W>(a.seen, i, lw) : load_piece<W>(a.seen, i, lw));
+    if (have_sv) {
+      sv.x = L.seen[lw * WPL];
+      if constexpr (WPL == 2) sv.y = L.seen[lw * WPL + 1];
+    } else {
+      sv = a.steer ? load_piece_nt<W>(a.seen, i, lw) : load_piece<W>(a.seen, i, lw);
+    }
     nw = acc & ~sv;
   }
   const uint32_t pc = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
@@ -316,12 +397,42 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
     if (lane == 0) a.fpop_next[v] = 0;
     return;
   }
+  const bool as_ids = (W >= 32) && a.ids_next != nullptr && tot <= (uint32_t)SPK;
+  if (as_ids) {   // compact the <= SPK new bits into a 64-byte id list (order is immaterial)
+    if (lane == 0) L.nids = 0;
+    wave_sync_lds();
+    uint32_t off = 0;
+    if (pc) off = atomicAdd(&L.nids, pc);
+    if (g == 0) {
+      u64 x = nw.x;
+      while (x) {
+        const int bb = __ffsll((long long)x) - 1;
+        x &= x - 1;
+        L.ids[off++] = (uint16_t)((lw * WPL) * 64 + bb);
+      }
+      if constexpr (WPL == 2) {
+        x = nw.y;
+        while (x) {
+          const int bb = __ffsll((long long)x) - 1;
+          x &= x - 1;
+          L.ids[off++] = (uint16_t)((lw * WPL + 1) * 64 + bb);
+        }
+      }
+    }
+    wave_sync_lds();
+    if (lane < SPK) a.ids_next[(size_t)v * SPK + lane] = lane < (int)tot ? L.ids[lane] : SP_EMPTY;
+    wave_sync_lds();
+    if (lane == 0) a.fmt_next[v] = 1;
+    st.add(S_SP_WRITTEN, 1);
+  } else if (a.fmt_next && lane == 0) {
+    a.fmt_next[v] = 0;
+  }
   if (g == 0) {
     if (a.steer) {
-      store_piece_nt<W>(a.next, v, lw, nw);
+      if (!as_ids) store_piece_nt<W>(a.next, v, lw, nw);
       if (nw.x | nw.y) store_piece_nt<W>(a.seen, i, lw, sv | nw);
     } else {
-      store_piece<W>(a.next, v, lw, nw);
+      if (!as_ids) store_piece<W>(a.next, v, lw, nw);
       if (nw.x | nw.y) store_piece<W>(a.seen, i, lw, sv | nw);
     }
     if (a.first) {
@@ -343,10 +454,27 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
     a.fpop_next[v] = tot;
     a.seenpop[i] += tot;
   }
-  st.c[S_NEW_BITS] += tot;
-  st.c[S_RECEIVERS] += 1;
-  st.c[S_WRITTEN] += 1;
-  st.c[S_NEXT_ARCS] += (u64)(uint32_t)max(a.deg_live[v], 0);
+  st.add(S_NEW_BITS, tot);
+  st.add(S_RECEIVERS, 1);
+  st.add(S_WRITTEN, 1);
+  st.add(S_NEXT_ARCS, (u64)(uint32_t)max(a.deg_live[v], 0));
+}
+
+// early exit: park the receiver's seen row in LDS (finish_row reuses it) and
+// return, in group-0 lanes, the messages of its component it still lacks
+template <int W>
+__device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, int64_t i, WaveLds& L, int g,
+                                                   int lw) {
+  constexpr int WPL = Geo<W>::WPL;
+  u64x2 want = {0, 0};
+  if (g == 0) {
+    const u64x2 sv = a.steer ? load_piece_nt<W>(a.seen, i, lw) : load_piece<W>(a.seen, i, lw);
+    const u64x2 cm = load_piece<W>(a.cmask, a.midx[v], lw);
+    L.seen[lw * WPL] = sv.x;
+    if constexpr (WPL == 2) L.seen[lw * WPL + 1] = sv.y;
+    want = cm & ~sv;
+  }
+  return want;
 }
 
 __device__ __forceinline__ u64 wave_sum_u64(u64 x) {
@@ -362,7 +490,7 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 x) {
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
-  __shared__ int32_t s_idx[WAVES][64];
+  __shared__ WaveLds s_w[WAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
@@ -373,40 +501,35 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
     const int64_t li = base + lane;
     bool need = false, act = false;
     u64 sends = 0;
-    int64_t b = 0, e = 0;
     if (li < a.nloc) {
       const int v = (int)(a.vbegin + li);
       const uint32_t fp = a.fpop[v];
       act = fp != 0u;
       if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
-      b = a.row_ptr[v];
-      e = a.row_ptr[v + 1];
+      const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
       need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
       if (!need && !hub) a.fpop_next[v] = 0;
     }
-    st.c[S_SENDS] += wave_sum_u64(sends);
-    st.c[S_ACTIVE] += (u64)__popcll(__ballot(act));
+    st.add(S_SENDS, wave_sum_u64(sends));
+    st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
     u64 m = __ballot(need);
     while (m) {
       const int k = __ffsll((long long)m) - 1;
       m &= m - 1;
       const int64_t i = base + k;
-      const int v = (int)(a.vbegin + i);
-      const int64_t vb = __shfl(b, k), ve = __shfl(e, k);
-      st.c[S_VISITED] += 1;
+      const int v = uniform((int)(a.vbegin + i));
+      const int64_t vb = a.row_ptr[v], ve = a.row_ptr[v + 1];   // scalar loads
+      st.add(S_VISITED, 1);
       const bool ee = a.early_exit != 0;
-      u64x2 acc = {0, 0}, sv = {0, 0}, cm = {0, 0};
+      u64x2 acc = {0, 0}, want = {0, 0};
       if (ee) {
-        st.c[S_SEEN_READ] += 1;
-        if (g == 0) {
-          sv = a.steer ? load_piece_nt<W>(a.seen, i, lw) : load_piece<W>(a.seen, i, lw);
-          cm = load_piece<W>(a.cmask, a.midx[v], lw);
-        }
+        st.add(S_SEEN_READ, 1);
+        want = early_exit_target<W>(a, v, i, s_w[wib], g, lw);
       }
-      gather<W>(a, vb, ve, s_idx[wib], lane, g, lw, acc, st, ee, sv, cm);
+      gather<W>(a, vb, ve, s_w[wib], lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
-      finish_row<W>(a, v, i, acc, lane, g, lw, st, ee, sv);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], ee);
     }
   }
   flush_stats(st, a.partial);
@@ -416,7 +539,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
-  __shared__ int32_t s_idx[WAVES][64];
+  __shared__ WaveLds s_w[WAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
@@ -429,12 +552,9 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
     u64x2 acc = {0, 0};
     if (!(a.state[h.v] & ST_DOWN) && a.seenpop[i] < a.done_at[h.v]) {
       const bool ee = a.early_exit != 0;
-      u64x2 sv = {0, 0}, cm = {0, 0};
-      if (ee && g == 0) {
-        sv = load_piece<W>(a.seen, i, lw);
-        cm = load_piece<W>(a.cmask, a.midx[h.v], lw);
-      }
-      gather<W>(a, h.beg, h.end, s_idx[wib], lane, g, lw, acc, st, ee, sv, cm);
+      u64x2 want = {0, 0};
+      if (ee) want = early_exit_target<W>(a, h.v, i, s_w[wib], g, lw);
+      gather<W>(a, h.beg, h.end, s_w[wib], lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
     }
     const bool nz = __any((acc.x | acc.y) != 0);
@@ -448,6 +568,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
+  __shared__ WaveLds s_w[WAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
@@ -460,14 +581,14 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
     if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= a.done_at[v]) {
       if (lane == 0) a.fpop_next[v] = 0;
     } else {
-      st.c[S_VISITED] += 1;
+      st.add(S_VISITED, 1);
       u64x2 acc = {0, 0};
       const int p0 = a.hub_item_ptr[h], p1 = a.hub_item_ptr[h + 1];
       if (g == 0) {
         for (int p = p0; p < p1; ++p)
           if (a.hub_pnz[p]) acc |= load_piece<W>(a.hub_partial, p, lw);
       }
-      finish_row<W>(a, v, i, acc, lane, g, lw, st);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib]);
     }
   }
   flush_stats(st, a.partial);
@@ -574,7 +695,19 @@ template <int W>
 __device__ __forceinline__ int stage_row(const ExpandArgs& a, int32_t u, u64* __restrict__ srow,
                                          int8_t* __restrict__ swords, int lane) {
   u64 x = 0;
-  if (lane < W) x = a.front[(size_t)u * W + lane];
+  if (W >= 32 && a.ids && a.fmt[u]) {   // id-list row: rebuild the words through LDS
+    if (lane < W) srow[lane] = 0ull;
+    wave_sync_lds();
+    if (lane < SPK) {
+      const uint16_t id = a.ids[(size_t)u * SPK + lane];
+      if (id != SP_EMPTY) atomicOr(&srow[id >> 6], 1ull << (id & 63));
+    }
+    wave_sync_lds();
+    if (lane < W) x = srow[lane];
+    wave_sync_lds();
+  } else if (lane < W) {
+    x = a.front[(size_t)u * W + lane];
+  }
   const u64 nzm = __ballot(x != 0ull);
   if (lane < W) srow[lane] = x;
   if (x) swords[lane_rank(nzm)] = (int8_t)lane;
@@ -586,8 +719,8 @@ __device__ __forceinline__ int stage_row(const ExpandArgs& a, int32_t u, u64* __
 
 __device__ __forceinline__ void push_sender_stats(const ExpandArgs& a, int32_t u, WaveStats& st) {
   if (u >= a.vbegin && u < a.vbegin + a.nloc) {
-    st.c[S_SENDS] += (u64)a.fpop[u] * (u64)(uint32_t)max(a.deg_live[u], 0);
-    st.c[S_ACTIVE] += 1;
+    st.add(S_SENDS, (u64)a.fpop[u] * (u64)(uint32_t)max(a.deg_live[u], 0));
+    st.add(S_ACTIVE, 1);
   }
 }
 
@@ -607,9 +740,10 @@ __global__ __launch_bounds__(BLOCK) void k_push(ExpandArgs a) {
     push_sender_stats(a, u, st);
     const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
     const int64_t jb = a.orp[u], je = a.orp[u + 1];
-    st.c[S_GATHERED] += 1;
-    st.c[S_ARCS] += (u64)(je - jb);
-    st.c[S_ATOMICS] += (u64)(je - jb) * (u64)nnz;
+    st.add(S_GATHERED, 1);
+    if (W >= 32 && a.ids && a.fmt[u]) st.add(S_SP_GATHERED, 1);
+    st.add(S_ARCS, (u64)(je - jb));
+    st.add(S_ATOMICS, (u64)(je - jb) * (u64)nnz);
     push_arcs<W>(a, jb, je, s_row[wib], s_words[wib], nnz, lane);
     __builtin_amdgcn_wave_barrier();
   }
@@ -637,14 +771,14 @@ __global__ __launch_bounds__(BLOCK) void k_push_big(ExpandArgs a) {
     const int64_t c0 = ((gw - (k * 7919) % nw) % nw + nw) % nw;   // first chunk of this wave
     if (c0 == 0 && gw == (k * 7919) % nw) {
       push_sender_stats(a, u, st);
-      st.c[S_GATHERED] += 1;
+      st.add(S_GATHERED, 1);
     }
     if (c0 >= nch) continue;
     const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
     for (int64_t c = c0; c < nch; c += nw) {
       const int64_t cb = jb + c * PUSH_CHUNK, ce = min(je, cb + PUSH_CHUNK);
-      st.c[S_ARCS] += (u64)(ce - cb);
-      st.c[S_ATOMICS] += (u64)(ce - cb) * (u64)nnz;
+      st.add(S_ARCS, (u64)(ce - cb));
+      st.add(S_ATOMICS, (u64)(ce - cb) * (u64)nnz);
       push_arcs<W>(a, cb, ce, s_row[wib], s_words[wib], nnz, lane);
     }
     __builtin_amdgcn_wave_barrier();
@@ -656,6 +790,7 @@ __global__ __launch_bounds__(BLOCK) void k_push_big(ExpandArgs a) {
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
+  __shared__ WaveLds s_w[WAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
@@ -671,21 +806,27 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
       acc = load_piece<W>(a.acc, v, lw);
       store_piece<W>(a.acc, v, lw, u64x2{0, 0});
     }
-    st.c[S_VISITED] += 1;
-    finish_row<W>(a, v, i, acc, lane, g, lw, st);
+    st.add(S_VISITED, 1);
+    finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib]);
   }
   flush_stats(st, a.partial);
 }
 
 // frontier activity bitmap: bit v of abits = (fpop[v] != 0); one wave per 64 vertices
-__global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, u64* __restrict__ abits,
-                                                  int64_t n) {
+__global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop,
+                                                  const uint8_t* __restrict__ fmt, u64* __restrict__ abits,
+                                                  u64* __restrict__ sbits, int64_t n) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
     const int64_t v = v0 + lane;
-    const u64 m = __ballot(v < n && fpop[v] != 0u);
-    if (lane == 0) abits[v0 >> 6] = m;
+    const bool on = v < n && fpop[v] != 0u;
+    const u64 m = __ballot(on);
+    const u64 sm = __ballot(on && fmt && fmt[v] != 0);
+    if (lane == 0) {
+      abits[v0 >> 6] = m;
+      sbits[v0 >> 6] = sm;
+    }
   }
 }
 
@@ -752,6 +893,8 @@ __global__ void k_done_at(const int32_t* __restrict__ comp, const uint32_t* __re
 // replicated on every rank, so every rank applies every group; the owner of
 // the origin also updates its Message-List, first-receipt and counters.
 struct InjectArgs {
+  const uint16_t* __restrict__ ids;    // id lists of frontier_r (null: dense only)
+  uint8_t* __restrict__ fmt;
   const int32_t* __restrict__ origin;
   const u64* __restrict__ bits;
   const uint32_t* __restrict__ cnt;
@@ -780,18 +923,29 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
     const int o = a.origin[gi];
     const bool owned = o >= a.vbegin && o < a.vend;
     if (a.state[o] & ST_DOWN) {
-      if (owned) st.c[S_LOST] += a.cnt[gi];
+      if (owned) st.add(S_LOST, a.cnt[gi]);
     } else {
       const uint32_t fp = a.fpop[o];
+      const bool was_ids = fp && a.ids && a.fmt[o];
       u64 b = 0, f = 0;
       if (lane < a.words) {
         b = a.bits[gi * a.words + lane];
-        f = fp ? a.front[(size_t)o * a.words + lane] : 0ull;
+        if (was_ids) {   // the row is an id list: rebuild its word for this lane
+          for (int q = 0; q < SPK; ++q) {
+            const uint16_t id = a.ids[(size_t)o * SPK + q];
+            if (id != SP_EMPTY && (id >> 6) == lane) f |= 1ull << (id & 63);
+          }
+        } else if (fp) {
+          f = a.front[(size_t)o * a.words + lane];
+        }
         f |= b;
         a.front[(size_t)o * a.words + lane] = f;
       }
       const uint32_t tot = wave_sum_u32((uint32_t)__popcll(f));
-      if (lane == 0) a.fpop[o] = tot;
+      if (lane == 0) {
+        a.fpop[o] = tot;
+        if (a.fmt) a.fmt[o] = 0;   // injected rows are dense
+      }
       if (owned) {
         const int64_t i = o - a.vbegin;
         if (lane < a.words) {
@@ -805,7 +959,7 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
           if (lane == 0) a.digest[i] ^= t;
         }
         if (lane == 0) a.seenpop[i] += nb;
-        st.c[S_INJECTED] += a.cnt[gi];
+        st.add(S_INJECTED, a.cnt[gi]);
       }
     }
   }
@@ -840,6 +994,7 @@ struct LiveArgs {
 __global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
   WaveStats st;
   ws_zero(st);
+  u64 ncrash = 0;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t v = (int64_t)blockIdx.x * BLOCK + threadIdx.x; v < a.n; v += stride) {
     uint8_t s = a.state[v];
@@ -850,7 +1005,7 @@ __global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
       if (crash) {
         s = (uint8_t)((s | ST_CRASHED) & ~ST_PENDING);
         a.fpop[v] = 0;   // crash-stop: its frontier is never sent
-        if (v >= a.vbegin && v < a.vend) st.c[S_CRASHED] += 1;
+        if (v >= a.vbegin && v < a.vend) ncrash += 1;
       }
     }
     if (s & ST_CRASHED) {
@@ -864,11 +1019,11 @@ __global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
     }
     a.state[v] = s;
   }
-  // crashed counts: wave-reduce then flush (lanes hold different values here)
-  u64 c = st.c[S_CRASHED];
+  // crash counts differ per lane: wave-reduce, then one uniform add
+  u64 c = ncrash;
 #pragma unroll
   for (int s = 32; s > 0; s >>= 1) c += __shfl_xor(c, s);
-  st.c[S_CRASHED] = c;
+  st.add(S_CRASHED, c);
   flush_stats(st, a.partial);
 }
 
@@ -897,9 +1052,9 @@ __global__ __launch_bounds__(BLOCK) void k_detect(LiveArgs a) {
     if (lane == 0) a.state[v] |= ST_REMOVED;
     for (int64_t j = b + lane; j < e; j += 64) atomicSub(&a.deg_live[a.col[j]], 1);
     if (v >= a.vbegin && v < a.vend) {
-      st.c[S_REPORTS] += tot;
-      st.c[S_REMOVALS] += 1;
-      st.c[S_DUP] += tot - 1;
+      st.add(S_REPORTS, tot);
+      st.add(S_REMOVALS, 1);
+      st.add(S_DUP, tot - 1);
       for (int pass = 0; pass < 2; ++pass) {
         const int32_t* cl = pass == 0 ? a.col : a.out_col;
         const int64_t pb = pass == 0 ? b : ob, pe = pass == 0 ? e : oe;
@@ -932,6 +1087,8 @@ __global__ __launch_bounds__(BLOCK) void k_detect(LiveArgs a) {
 // over rows [0, count).  Lane l holds word l % W of vertex slot l / W; each lane
 // keeps 64 register counters per output.
 struct BitsumArgs {
+  const uint16_t* __restrict__ ids;   // optional id-list rows [count][SPK] (with fmt)
+  const uint8_t* __restrict__ fmt;
   const u64* __restrict__ rows;       // [count][W]
   const uint32_t* __restrict__ guard; // optional: row valid iff guard[i] != 0
   const int32_t* __restrict__ weight; // [count]
@@ -961,8 +1118,17 @@ __global__ __launch_bounds__(BLOCK) void k_bitsum(BitsumArgs a) {
   }
   const int64_t step = (int64_t)gridDim.x * WAVES * VPS;
   for (int64_t i = ((int64_t)blockIdx.x * WAVES + wib) * VPS + q; i < a.count; i += step) {
-    u64 x = a.rows[i * W + w];
-    if (a.guard && a.guard[i] == 0) x = 0;
+    u64 x = 0;
+    if (!a.guard || a.guard[i] != 0) {
+      if (a.fmt && a.fmt[i]) {
+        for (int q = 0; q < SPK; ++q) {
+          const uint16_t id = a.ids[i * SPK + q];
+          if (id != SP_EMPTY && (id >> 6) == w) x |= 1ull << (id & 63);
+        }
+      } else {
+        x = a.rows[i * W + w];
+      }
+    }
     const uint32_t wt = SUM ? (uint32_t)max(a.weight[i], 0) : 0u;
 #pragma unroll
     for (int b = 0; b < 64; ++b) {
@@ -1014,6 +1180,11 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.front = c->d_front[c->cur];
   a.fpop = c->d_fpop[c->cur];
   a.abits = c->d_abits;
+  a.sbits = c->d_sbits;
+  a.ids = c->d_ids[c->cur];
+  a.fmt = c->d_fmt[c->cur];
+  a.ids_next = c->d_ids[c->cur ^ 1];
+  a.fmt_next = c->d_fmt[c->cur ^ 1];
   a.done_at = c->d_done_at;
   a.gcol = c->d_gcol;
   a.midx = c->d_midx;
@@ -1083,7 +1254,8 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 
 static int launch_expand(Ctx* c) {
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
-                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc);
+                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_ids[0] ? c->d_fmt[c->cur] : nullptr,
+                     c->d_abits, c->d_sbits, c->n_alloc);
   // direction: push when the senders' arcs are a small share of all arcs
   const int r = c->round;
   // early exit pays once frontier rows are dense: >= m/16 new bits per vertex last round
@@ -1186,6 +1358,8 @@ static void free_state(Ctx* c) {
   dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_done_at);
+  dfree(&c->d_sbits);
+  for (int k = 0; k < 2; ++k) { dfree(&c->d_ids[k]); dfree(&c->d_fmt[k]); }
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
@@ -1237,6 +1411,17 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_deg_live, na));
   GP_TRY(dalloc(&c->d_cand, na));
   GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
+  GP_TRY(dalloc(&c->d_sbits, (na + 63) / 64));
+  for (int k = 0; k < 2; ++k) {
+    if (W >= 32 && c->cfg.sparse_rows) {
+      GP_TRY(dalloc(&c->d_ids[k], na * SPK));
+      GP_TRY(dalloc(&c->d_fmt[k], na));
+      GP_HIP(hipMemset(c->d_fmt[k], 0, na));
+    } else {
+      dfree(&c->d_ids[k]);
+      dfree(&c->d_fmt[k]);
+    }
+  }
   GP_TRY(dalloc(&c->d_done_at, na));
   c->done_at_valid = false;
   GP_TRY(dalloc(&c->d_acc, na * W));
@@ -1345,6 +1530,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->push_ratio = 40.0;   // push when sender arcs <= nnz / 40
   cfg->early_exit = 1;
   cfg->hot_degree = 0;
+  cfg->sparse_rows = 1;
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -1381,6 +1567,8 @@ void gp_destroy(gp_ctx* c) {
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
   dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_done_at);
+  dfree(&c->d_sbits);
+  for (int k = 0; k < 2; ++k) { dfree(&c->d_ids[k]); dfree(&c->d_fmt[k]); }
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -1677,6 +1865,8 @@ static int round_launch(Ctx* c) {
     ia.cnt = c->d_inj_cnt;
     ia.front = c->d_front[c->cur];
     ia.fpop = c->d_fpop[c->cur];
+    ia.ids = c->d_ids[c->cur];
+    ia.fmt = c->d_ids[0] ? c->d_fmt[c->cur] : nullptr;
     ia.seen = c->d_seen;
     ia.seenpop = c->d_seenpop;
     ia.first = c->cfg.track_first ? c->d_first : nullptr;
@@ -1697,6 +1887,8 @@ static int round_launch(Ctx* c) {
     BitsumArgs b{};
     b.rows = c->d_front[c->cur] + (size_t)c->vbegin * c->words;
     b.guard = c->d_fpop[c->cur] + c->vbegin;
+    b.ids = c->d_ids[0] ? c->d_ids[c->cur] + (size_t)c->vbegin * SPK : nullptr;
+    b.fmt = c->d_ids[0] ? c->d_fmt[c->cur] + c->vbegin : nullptr;
     b.weight = c->d_deg_live + c->vbegin;
     b.cnt = nullptr;
     b.wsum = c->d_msg_fwd;
@@ -1724,6 +1916,12 @@ static int round_exchange_rccl(Ctx* c) {
                         (size_t)c->slice * W, ncclUint64, c->comm, s));
   GP_RCCL(ncclAllGather(c->d_fpop[nx] + (size_t)c->rank * c->slice, c->d_fpop[nx],
                         (size_t)c->slice, ncclUint32, c->comm, s));
+  if (c->d_ids[0]) {
+    GP_RCCL(ncclAllGather(c->d_ids[nx] + (size_t)c->rank * c->slice * SPK, c->d_ids[nx],
+                          (size_t)c->slice * SPK * 2, ncclUint8, c->comm, s));
+    GP_RCCL(ncclAllGather(c->d_fmt[nx] + (size_t)c->rank * c->slice, c->d_fmt[nx], (size_t)c->slice,
+                          ncclUint8, c->comm, s));
+  }
   // the report cursor (slot S_REPORT_CURSOR) stays rank-local
   GP_RCCL(ncclAllReduce(c->d_stats, c->d_stats, S_REPORT_CURSOR, ncclUint64, ncclSum, c->comm, s));
   GP_RCCL(ncclGroupEnd());
@@ -1756,6 +1954,8 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->rows_written = h[S_WRITTEN];
     out->vertices_visited = h[S_VISITED];
     out->atomics = h[S_ATOMICS];
+    out->sparse_gathered = h[S_SP_GATHERED];
+    out->sparse_written = h[S_SP_WRITTEN];
     out->next_arcs = h[S_NEXT_ARCS];
     out->mode = c->mode_push ? 1 : 0;
     out->overflow = (int64_t)h[S_REPORT_CURSOR] > c->report_cap ? 1 : 0;
@@ -1816,6 +2016,12 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
                             (size_t)(e - b) * W * 8, hipMemcpyDefault, dst->stream));
       GP_HIP(hipMemcpyAsync(dst->d_fpop[nx] + b, src->d_fpop[src->cur ^ 1] + b, (size_t)(e - b) * 4,
                             hipMemcpyDefault, dst->stream));
+      if (dst->d_ids[0] && src->d_ids[0]) {
+        GP_HIP(hipMemcpyAsync(dst->d_ids[nx] + (size_t)b * SPK, src->d_ids[src->cur ^ 1] + (size_t)b * SPK,
+                              (size_t)(e - b) * SPK * 2, hipMemcpyDefault, dst->stream));
+        GP_HIP(hipMemcpyAsync(dst->d_fmt[nx] + b, src->d_fmt[src->cur ^ 1] + b, (size_t)(e - b),
+                              hipMemcpyDefault, dst->stream));
+      }
     }
   }
   gp_round_stats sum;
@@ -1832,6 +2038,7 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     sum.rows_gathered += st.rows_gathered; sum.seen_rows_read += st.seen_rows_read;
     sum.rows_written += st.rows_written; sum.vertices_visited += st.vertices_visited;
     sum.atomics += st.atomics; sum.next_arcs += st.next_arcs; sum.mode = st.mode;
+    sum.sparse_gathered += st.sparse_gathered; sum.sparse_written += st.sparse_written;
     sum.expand_ms = std::max(sum.expand_ms, st.expand_ms);
     sum.exchange_ms = std::max(sum.exchange_ms, st.exchange_ms);
     sum.round_ms = std::max(sum.round_ms, st.round_ms);
@@ -1966,8 +2173,25 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       GP_HIP(hipMemcpy(fp.data(), c->d_fpop[c->cur], (size_t)n * 4, hipMemcpyDeviceToHost));
       GP_HIP(hipMemcpy(host, c->d_front[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
       uint64_t* h = static_cast<uint64_t*>(host);
-      for (int64_t v = 0; v < n; ++v)
-        if (!fp[v]) std::memset(h + v * W, 0, (size_t)W * 8);
+      std::vector<uint8_t> fm;
+      std::vector<uint16_t> ids;
+      if (c->d_ids[0]) {
+        fm.resize((size_t)n);
+        ids.resize((size_t)n * SPK);
+        GP_HIP(hipMemcpy(fm.data(), c->d_fmt[c->cur], (size_t)n, hipMemcpyDeviceToHost));
+        GP_HIP(hipMemcpy(ids.data(), c->d_ids[c->cur], (size_t)n * SPK * 2, hipMemcpyDeviceToHost));
+      }
+      for (int64_t v = 0; v < n; ++v) {
+        if (!fp[v]) {
+          std::memset(h + v * W, 0, (size_t)W * 8);
+        } else if (!fm.empty() && fm[(size_t)v]) {
+          std::memset(h + v * W, 0, (size_t)W * 8);
+          for (int q = 0; q < SPK; ++q) {
+            const uint16_t id = ids[(size_t)v * SPK + q];
+            if (id != SP_EMPTY) h[v * W + (id >> 6)] |= 1ull << (id & 63);
+          }
+        }
+      }
       return 0;
     }
     default:

@@ -22,7 +22,7 @@ typedef unsigned long long u64;
 enum StatSlot {
   S_INJECTED = 0, S_LOST, S_NEW_BITS, S_RECEIVERS, S_SENDS, S_ACTIVE, S_CRASHED,
   S_REPORTS, S_REMOVALS, S_DUP, S_ARCS, S_GATHERED, S_SEEN_READ, S_WRITTEN,
-  S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_RESERVED, NST,
+  S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_SP_GATHERED, S_SP_WRITTEN, NST,
   S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR
 };
 
@@ -80,6 +80,9 @@ struct Ctx {
   int32_t* d_deg_live = nullptr;    // [n_alloc]
   int32_t* d_cand = nullptr;        // [n] detection candidates of a round
   u64* d_abits = nullptr;           // [n_alloc/64] frontier activity bitmap
+  u64* d_sbits = nullptr;           // [n_alloc/64] frontier rows held as id lists
+  uint16_t* d_ids[2] = {nullptr, nullptr};   // [n_alloc][32] id-list rows (W >= 32 only)
+  uint8_t* d_fmt[2] = {nullptr, nullptr};    // [n_alloc] 1 = id-list row
   // push (sparse-round) mode
   u64* d_acc = nullptr;             // [n_alloc][W] OR accumulator, kept all-zero between uses
   u64* d_tbits = nullptr;           // [n_alloc/64] receivers pushed to this round

@@ -71,6 +71,8 @@ typedef struct gp_round_stats {
   uint64_t vertices_visited;/* receivers whose in-list was scanned                   */
   uint64_t atomics;         /* push mode: 64-bit atomicOr issued                      */
   uint64_t next_arcs;       /* out-degree sum of this round's receivers (direction)   */
+  uint64_t sparse_gathered; /* frontier rows read in id-list form (64 B each)        */
+  uint64_t sparse_written;  /* next rows written in id-list form                     */
   int32_t mode;             /* 0 = pull expansion, 1 = push expansion                 */
   int32_t pad;
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
@@ -100,6 +102,8 @@ typedef struct gp_config {
   int32_t early_exit;          /* coverage-checked pull scans in dense rounds (§3.4)   */
   int32_t hot_degree;          /* > 0: rows of vertices with in-degree >= hot_degree are
                                   loaded cacheable, all other streams non-temporal (§3.5) */
+  int32_t sparse_rows;         /* W >= 32: rows with <= 32 new bits stored as id lists */
+  int32_t pad;
 } gp_config;
 
 /* what for gp_read */

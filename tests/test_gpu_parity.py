@@ -31,11 +31,11 @@ MODES = [0.0, 1e-12, 10.0]
 
 
 def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096,
-             push_ratio=10.0, **kw):
+             push_ratio=10.0, sparse_rows=1, **kw):
     churn = kw.get("churn", False)
     cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(bool(churn or crashes)),
                churn=int(churn), p_fail=kw.get("p_fail", 0.0), churn_seed=kw.get("churn_seed", 0),
-               hub_threshold=hub_threshold, push_ratio=push_ratio)
+               hub_threshold=hub_threshold, push_ratio=push_ratio, sparse_rows=sparse_rows)
     eng = _engine(pkg, g, origin, inject, **cfg)
     by_round = {}
     for v, r in crashes:
@@ -245,3 +245,27 @@ def test_full_size_invariants_c3(pkg):
     assert [x["new_bits"] for x in s1] == [x["new_bits"] for x in s2]
     assert sum(x["sends"] for x in s1) == int(fwd.sum())
     assert sum(x["new_bits"] + x["injected"] for x in s1) == int(cov.sum())
+
+
+@pytest.mark.parametrize("sparse_rows", [0, 1])
+@pytest.mark.parametrize("push_ratio", MODES)
+def test_wide_rows_sparse_format(pkg, oracle, push_ratio, sparse_rows):
+    """W = 64 (4096 messages) with id-list frontier rows on and off, injections
+    spread over rounds, churn: exercises id lists through pull, push, injection
+    into an id-list row and per-message forwards."""
+    rp, col = oracle.chung_lu(60_000, 10, 2.4, 21)
+    g = pkg.CSR(60_000, rp, col, False)
+    m = 4096
+    origin = pkg.overlay.random_origins(g.n, m, seed=21)
+    inject = (np.arange(m) % 6).astype(np.int32)
+    cfg_first = push_ratio != 10.0   # first matrix on two of the three modes (1 GB host copy otherwise)
+    churn = dict(churn=True, p_fail=0.01, churn_seed=5)
+    eng_cfg = dict(push_ratio=push_ratio)
+    r = _compare(pkg, oracle, g, origin, inject, first=cfg_first, hub_threshold=512,
+                 sparse_rows=sparse_rows, **eng_cfg, **churn)
+    if sparse_rows:
+        assert sum(s["sparse_written"] for s in r["stats"]) > 0
+        assert sum(s["sparse_gathered"] for s in r["stats"]) > 0
+    else:
+        assert sum(s["sparse_written"] for s in r["stats"]) == 0
+    r["eng"].close()
