@@ -42,6 +42,10 @@ def parse():
                     help="cache-steer rows of vertices with in-degree >= this (0 = off)")
     ap.add_argument("--push-ratio", type=float, default=40.0)
     ap.add_argument("--early-exit", type=int, default=1)
+    ap.add_argument("--unfiltered-pct", type=int, default=90,
+                    help="pull without the per-arc activity check when >= this %% of vertices send (0 = never)")
+    ap.add_argument("--sparse-rows", type=int, default=0,
+                    help="store frontier rows with <= 32 new bits as id lists (W >= 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-messages", type=int, default=64)
@@ -50,14 +54,21 @@ def parse():
     return ap.parse_args()
 
 
+SPARSE_ROW_BYTES = 64   # id-list row: 32 u16 message ids
+
+
 def round_bytes(st, words, nloc):
     """Algorithmic bytes of one expansion launch of the sparse-aware pull
-    (DESIGN.md §4): per owned vertex 21 B of vertex state, per scanned arc 8 B
-    (column id + the neighbour's frontier popcount), per gathered frontier row
-    8W B, per receiver seen row read 8W B, per written row 16W B (next + seen)."""
+    (DESIGN.md §3.2): per owned vertex 21 B of vertex state, per scanned arc 8 B
+    (column id + the neighbour's activity bit), per gathered frontier row 8W B
+    (64 B when it is an id list), per receiver seen row read 8W B, per written
+    row 8W B of seen plus 8W B of next (64 B when next is an id list)."""
     w8 = 8 * words
-    return (21 * nloc + 8 * st["arcs_scanned"] + w8 * (st["rows_gathered"] + st["seen_rows_read"])
-            + 2 * w8 * st["rows_written"])
+    sg, sw = st.get("sparse_gathered", 0), st.get("sparse_written", 0)
+    gathered = w8 * (st["rows_gathered"] - sg) + SPARSE_ROW_BYTES * sg
+    written = w8 * st["rows_written"] + w8 * (st["rows_written"] - sw) + SPARSE_ROW_BYTES * sw
+    arc = 4 if st.get("unfiltered") else 8   # column id (+ activity-bitmap probe when filtered)
+    return 21 * nloc + arc * st["arcs_scanned"] + gathered + w8 * st["seen_rows_read"] + written
 
 
 def dense_round_bytes(n, nnz, words):
@@ -93,7 +104,8 @@ def main():
     n = 1 << args.log2n
     eng = pkg.GossipEngine(local, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
                            hot_degree=args.hot_degree, push_ratio=args.push_ratio,
-                           early_exit=args.early_exit)
+                           early_exit=args.early_exit, sparse_rows=args.sparse_rows,
+                           unfiltered_pct=args.unfiltered_pct)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()
@@ -125,16 +137,21 @@ def main():
     rounds = sum(len(r) for r in runs)
     exp_ms = sum(s["expand_ms"] for r in runs for s in r)
     exch_ms = sum(s["exchange_ms"] for r in runs for s in r)
-    nbytes = sum(round_bytes(s, eng.words, n) for r in runs for s in r)
+    # roofline of the dominant kernel, k_expand: its pull rounds only, its own
+    # HIP-event time (kernel_ms); alg bytes include the small hub passes' share
+    pulls = [s for r in runs for s in r if s["mode"] == 0 and s["kernel_ms"] > 0]
+    nbytes = sum(round_bytes(s, eng.words, n) for s in pulls)
+    kern_ms = sum(s["kernel_ms"] for s in pulls)
     if world > 1:   # counters are global (all-reduced): per-rank share for the per-GPU roofline
         nbytes /= world
-    achieved = nbytes / (exp_ms * 1e-3) / 1e9 if exp_ms > 0 else 0.0
+    achieved = nbytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     dense_eq = dense_round_bytes(n, nnz, eng.words) * rounds / world / (exp_ms * 1e-3) / 1e9
     if args.profile_steps and rank == 0:
         for s in runs[-1]:
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
-                                                "rows_written", "atomics", "expand_ms", "exchange_ms")}),
+                                                "rows_written", "sparse_gathered", "sparse_written", "atomics",
+                                                "unfiltered", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -161,9 +178,11 @@ def main():
                        "setup_s": round(setup_s, 2)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": f"k_expand<{eng.words}> (+hub passes), HIP events on the engine stream",
-                         "avg_launch_ms": exp_ms / rounds,
-                         "alg_bytes_per_launch": nbytes / rounds,
+                         "kernel": f"k_expand<{eng.words}>, HIP events on the engine stream",
+                         "launches": len(pulls),
+                         "avg_launch_ms": kern_ms / max(len(pulls), 1),
+                         "alg_bytes_per_launch": nbytes / max(len(pulls), 1),
+                         "expand_ms_per_step": exp_ms / args.steps,
                          "dense_equivalent_GBs": dense_eq,
                          "exchange_ms_per_round": exch_ms / rounds},
             "cpu_baseline": cpu,

@@ -50,10 +50,11 @@ class RoundStats(ctypes.Structure):
         ("sparse_gathered", ctypes.c_uint64),
         ("sparse_written", ctypes.c_uint64),
         ("mode", ctypes.c_int32),
-        ("pad", ctypes.c_int32),
+        ("unfiltered", ctypes.c_int32),
         ("expand_ms", ctypes.c_double),
         ("exchange_ms", ctypes.c_double),
         ("round_ms", ctypes.c_double),
+        ("kernel_ms", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -79,7 +80,7 @@ class Config(ctypes.Structure):
         ("early_exit", ctypes.c_int32),
         ("hot_degree", ctypes.c_int32),
         ("sparse_rows", ctypes.c_int32),
-        ("pad", ctypes.c_int32),
+        ("unfiltered_pct", ctypes.c_int32),
     ]
 
 
@@ -114,6 +115,7 @@ SIGNATURES = {
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
 }
 
+ABI_VERSION = 2   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 
@@ -138,6 +140,8 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.gp_abi_version() != ABI_VERSION:
+        raise GossipLibraryError(f"{path}: ABI {lib.gp_abi_version()} != expected {ABI_VERSION}; rebuild it")
     _lib = lib
     return lib
 

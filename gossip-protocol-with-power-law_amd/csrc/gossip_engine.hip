@@ -187,6 +187,7 @@ struct ExpandArgs {
   const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
   int32_t early_exit;                  // this round scans with the coverage check
+  int32_t unfiltered;                  // read every in-neighbour row (inactive rows are zero)
   int32_t steer;                       // nt loads/stores for streamed data, cached hub rows
   const uint32_t* __restrict__ done_at;// |messages of v's component|: seenpop == done_at -> done
   u64* __restrict__ next;
@@ -291,8 +292,12 @@ __device__ __forceinline__ void gather(const ExpandArgs& a, int64_t b, int64_t e
     if (lane < n) {
       tu = a.steer ? __builtin_nontemporal_load(a.gcol + j0 + lane) : a.gcol[j0 + lane];
       const int32_t u = tu & 0x7FFFFFFF;
-      act = (a.abits[u >> 6] >> (u & 63)) & 1ull;
-      if (act && sparse_ok) spr = (a.sbits[u >> 6] >> (u & 63)) & 1ull;
+      if (a.unfiltered) {   // dense round: no bitmap probe (it misses L2 under the row stream)
+        act = true;
+      } else {
+        act = (a.abits[u >> 6] >> (u & 63)) & 1ull;
+        if (act && sparse_ok) spr = (a.sbits[u >> 6] >> (u & 63)) & 1ull;
+      }
     }
     const u64 dmask = __ballot(act && !spr);
     const u64 smask = __ballot(spr);
@@ -830,6 +835,38 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
   }
 }
 
+// unfiltered rounds: make every frontier row readable without
+// the activity check -- rows of inactive vertices (fpop == 0: never written,
+// or crashed) become zero, id-list rows are expanded to bitmap rows.  One wave
+// per 64-vertex bitmap word; fully active dense words cost one load.
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64* __restrict__ abits, const u64* __restrict__ sbits,
+                                                      const uint16_t* __restrict__ ids, uint8_t* __restrict__ fmt,
+                                                      u64* __restrict__ front, int64_t n_alloc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (w * 64 >= n_alloc) return;
+  const u64 sp = (ids != nullptr) ? sbits[w] : 0ull;
+  u64 todo = ~abits[w] | sp;
+  while (todo) {
+    const int b = __ffsll((long long)todo) - 1;
+    todo &= todo - 1;
+    const int64_t v = w * 64 + b;
+    if (v >= n_alloc) break;
+    u64 x = 0;
+    if ((sp >> b) & 1ull) {
+      if constexpr (W >= 32) {
+        for (int q = 0; q < SPK; ++q) {
+          const uint16_t id = ids[(size_t)v * SPK + q];
+          if (id != SP_EMPTY && (id >> 6) == lane) x |= 1ull << (id & 63);
+        }
+      }
+      if (lane == 0) fmt[v] = 0;
+    }
+    if (lane < W) front[(size_t)v * W + lane] = x;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // weakly connected components (union-find, hook larger root under smaller,
 // so the label of a component is its smallest vertex id).  A vertex holding
@@ -1241,8 +1278,13 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     return;
   }
   const int64_t per_block = (int64_t)WAVES * 64;
+  if (a.unfiltered)
+    hipLaunchKernelGGL(k_fixup_rows<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
+                       c->d_abits, c->d_sbits, a.ids, c->d_fmt[c->cur], c->d_front[c->cur], c->n_alloc);
+  (void)hipEventRecord(c->ev[4], c->stream);
   if (a.nloc > 0)
     hipLaunchKernelGGL(k_expand<W>, dim3(grid_for(a.nloc, per_block)), dim3(BLOCK), 0, c->stream, a);
+  (void)hipEventRecord(c->ev[5], c->stream);
   if (c->n_hub_items > 0) {
     ExpandArgs h = a;
     h.n_items = c->n_hub_items;
@@ -1265,8 +1307,14 @@ static int launch_expand(Ctx* c) {
   c->mode_push = c->cfg.push_ratio > 0.0 && est * c->cfg.push_ratio <= (double)c->nnz;
   if (c->mode_push && c->nloc() > 0)
     GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1] + c->vbegin, 0, (size_t)c->nloc() * 4, c->stream));
+  // unfiltered pull when (nearly) every vertex is a sender: last round's
+  // receivers + this round's injected origins >= unfiltered_pct % of n
+  const double senders = (double)c->prev_receivers + (double)c->inj_groups_at(r);
+  c->unfiltered_now = !c->mode_push && c->cfg.unfiltered_pct > 0 &&
+                      senders * 100.0 >= (double)c->cfg.unfiltered_pct * (double)c->n;
   ExpandArgs a{};
   fill_expand(c, a);
+  a.unfiltered = c->unfiltered_now ? 1 : 0;
   switch (c->words) {
     case 1: launch_expand_w<1>(c, a); break;
     case 2: launch_expand_w<2>(c, a); break;
@@ -1530,7 +1578,8 @@ void gp_default_config(gp_config* cfg) {
   cfg->push_ratio = 40.0;   // push when sender arcs <= nnz / 40
   cfg->early_exit = 1;
   cfg->hot_degree = 0;
-  cfg->sparse_rows = 1;
+  cfg->sparse_rows = 0;
+  cfg->unfiltered_pct = 90;
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -1778,6 +1827,7 @@ int gp_reset(gp_ctx* c) {
   GP_HIP(hipMemsetAsync(c->d_tbits, 0, (na + 63) / 64 * 8, s));
   c->prev_next_arcs = 0;
   c->prev_new_bits = 0;
+  c->prev_receivers = 0;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
   GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToDevice, s));
@@ -1958,6 +2008,13 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->sparse_written = h[S_SP_WRITTEN];
     out->next_arcs = h[S_NEXT_ARCS];
     out->mode = c->mode_push ? 1 : 0;
+    out->unfiltered = (!c->mode_push && c->unfiltered_now) ? 1 : 0;
+    out->kernel_ms = 0.0;
+    if (!c->mode_push && c->nloc() > 0) {
+      float kms = 0.f;
+      (void)hipEventElapsedTime(&kms, c->ev[4], c->ev[5]);
+      out->kernel_ms = kms;
+    }
     out->overflow = (int64_t)h[S_REPORT_CURSOR] > c->report_cap ? 1 : 0;
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
@@ -1970,6 +2027,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   c->last_reports = (int64_t)h[S_REPORT_CURSOR];
   c->prev_next_arcs = h[S_NEXT_ARCS];
   c->prev_new_bits = h[S_NEW_BITS];
+  c->prev_receivers = h[S_RECEIVERS];
   c->cur ^= 1;
   c->round = r + 1;
   return 0;

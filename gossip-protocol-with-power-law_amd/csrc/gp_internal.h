@@ -94,6 +94,12 @@ struct Ctx {
   bool mode_push = false;           // direction of the current round
   bool early_exit_now = false;      // coverage-checked scan this round
   u64 prev_new_bits = 0;            // new bits of the last round (global)
+  u64 prev_receivers = 0;           // receivers of the last round (global)
+  bool unfiltered_now = false;      // this round's pull skips the activity check
+  int64_t inj_groups_at(int32_t r) const {
+    auto it = inject.find(r);
+    return it == inject.end() ? 0 : it->second.cnt;
+  }
   int32_t* d_gcol = nullptr;        // [nnz] in-CSR columns, rows sorted by neighbour degree desc
   int32_t* d_midx = nullptr;        // [n_alloc] component mask row of v (-1: none)
   u64* d_cmask = nullptr;           // [K][W] messages per component

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 1
+#define GP_ABI_VERSION 2
 
 typedef struct gp_ctx gp_ctx;
 
@@ -74,10 +74,12 @@ typedef struct gp_round_stats {
   uint64_t sparse_gathered; /* frontier rows read in id-list form (64 B each)        */
   uint64_t sparse_written;  /* next rows written in id-list form                     */
   int32_t mode;             /* 0 = pull expansion, 1 = push expansion                 */
-  int32_t pad;
+  int32_t unfiltered;       /* 1: the pull read every in-neighbour row without the
+                               per-arc activity-bitmap check (dense round, §3.4)     */
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
+  double kernel_ms;         /* device time of the main pull kernel k_expand alone    */
 } gp_round_stats;
 
 /* One dead-node report: reporter saw `dead` miss 3 heartbeats in `round`. */
@@ -103,7 +105,8 @@ typedef struct gp_config {
   int32_t hot_degree;          /* > 0: rows of vertices with in-degree >= hot_degree are
                                   loaded cacheable, all other streams non-temporal (§3.5) */
   int32_t sparse_rows;         /* W >= 32: rows with <= 32 new bits stored as id lists */
-  int32_t pad;
+  int32_t unfiltered_pct;      /* pull without the per-arc activity check when >= this %
+                                  of vertices are senders (0 = never)   */
 } gp_config;
 
 /* what for gp_read */
