@@ -38,8 +38,6 @@ def parse():
     ap.add_argument("--messages", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--hub-threshold", type=int, default=4096)
-    ap.add_argument("--hot-degree", type=int, default=0,
-                    help="cache-steer rows of vertices with in-degree >= this (0 = off)")
     ap.add_argument("--push-ratio", type=float, default=40.0)
     ap.add_argument("--early-exit", type=int, default=1)
     ap.add_argument("--unfiltered-pct", type=int, default=90,
@@ -103,7 +101,7 @@ def main():
     pg = dist.init("gloo")
     n = 1 << args.log2n
     eng = pkg.GossipEngine(local, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
-                           hot_degree=args.hot_degree, push_ratio=args.push_ratio,
+                           push_ratio=args.push_ratio,
                            early_exit=args.early_exit, sparse_rows=args.sparse_rows,
                            unfiltered_pct=args.unfiltered_pct)
     t0 = time.perf_counter()

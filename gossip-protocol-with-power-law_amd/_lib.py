@@ -78,7 +78,7 @@ class Config(ctypes.Structure):
         ("report_capacity", ctypes.c_int64),
         ("push_ratio", ctypes.c_double),
         ("early_exit", ctypes.c_int32),
-        ("hot_degree", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
         ("sparse_rows", ctypes.c_int32),
         ("unfiltered_pct", ctypes.c_int32),
     ]
@@ -115,7 +115,7 @@ SIGNATURES = {
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
 }
 
-ABI_VERSION = 2   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 3   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

@@ -63,34 +63,6 @@ __device__ __forceinline__ u64x2 load_piece(const u64* __restrict__ base, int64_
     return r;
   }
 }
-// non-temporal forms: streamed data that must not displace the hub rows the
-// gather re-reads from the Infinity Cache / L2
-template <int W>
-__device__ __forceinline__ u64x2 load_piece_nt(const u64* __restrict__ base, int64_t row, int lw) {
-  if constexpr (W >= 2) {
-    return __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(base + row * W + lw * 2));
-  } else {
-    u64x2 r;
-    r.x = __builtin_nontemporal_load(base + row);
-    r.y = 0;
-    return r;
-  }
-}
-template <int W>
-__device__ __forceinline__ void store_piece_nt(u64* __restrict__ base, int64_t row, int lw, u64x2 x) {
-  if constexpr (W >= 2) {
-    __builtin_nontemporal_store(x, reinterpret_cast<u64x2*>(base + row * W + lw * 2));
-  } else {
-    __builtin_nontemporal_store(x.x, base + row);
-  }
-}
-template <int W>
-__device__ __forceinline__ u64x2 load_row(const u64* __restrict__ base, int32_t tagged, int lw, bool steer) {
-  const int32_t u = tagged & 0x7FFFFFFF;
-  if (steer && tagged >= 0) return load_piece_nt<W>(base, u, lw);   // cold row
-  return load_piece<W>(base, u, lw);                                  // hub row: cacheable
-}
-
 template <int W>
 __device__ __forceinline__ void store_piece(u64* __restrict__ base, int64_t row, int lw, u64x2 x) {
   if constexpr (W >= 2) {
@@ -177,18 +149,13 @@ struct ExpandArgs {
   const int32_t* __restrict__ col;
   const u64* __restrict__ front;       // frontier_r
   const uint32_t* __restrict__ fpop;   // |frontier_r|
-  const u64* __restrict__ abits;       // bit v: frontier_r(v) != 0 (2 MB at 2^24: L2-resident)
-  const u64* __restrict__ sbits;       // bit v: frontier_r(v) stored as an id list
-  const uint16_t* __restrict__ ids;    // [n_alloc][SPK] id lists of frontier_r (null: dense only)
-  const uint8_t* __restrict__ fmt;     // [n_alloc] 1 = id list (valid iff fpop != 0)
-  uint16_t* __restrict__ ids_next;
-  uint8_t* __restrict__ fmt_next;
+  const u64x2* __restrict__ bits2;     // per 64 vertices {active: fpop != 0, list row: 1 <= fpop <= list_max}
+  int32_t list_max;                    // frontier rows with <= list_max bits are id lists (0: none)
   const int32_t* __restrict__ gcol;    // in-CSR columns in gather order (neighbour degree desc)
   const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
   int32_t early_exit;                  // this round scans with the coverage check
   int32_t unfiltered;                  // read every in-neighbour row (inactive rows are zero)
-  int32_t steer;                       // nt loads/stores for streamed data, cached hub rows
   const uint32_t* __restrict__ done_at;// |messages of v's component|: seenpop == done_at -> done
   u64* __restrict__ next;
   uint32_t* __restrict__ fpop_next;
@@ -221,23 +188,77 @@ struct ExpandArgs {
   int32_t vpw;                         // vertices per wave (k_expand)
 };
 
-// Sparse frontier rows: a row with at most SPK new bits is
-// written as a list of SPK u16 message ids (64 B, 0xFFFF = empty) instead of
-// the 8W-byte bitmap row; the gather ORs such rows into a per-wave LDS row with
-// ds_or_b64.  Only for W >= 32 (rows >= 256 B).
-constexpr int SPK = 32;
+// Id-list frontier rows: a row with 1 <= fpop <= LIST_MAX new
+// bits holds its message ids as u16 in the first 64 B of its own row slot
+// (0xFFFF-padded) instead of the 8W-byte bitmap; the format is a pure function
+// of fpop, so no side array travels with the rows.  The gather ORs list rows
+// into a per-wave LDS row with ds_or_b64.  Only for W >= 16 (rows >= 128 B).
+constexpr int LIST_SLOTS = 32;   // u16 slots of one 64-byte list segment
+// occupancy target of k_expand (waves per SIMD; 0 = compiler's choice)
+#ifndef GP_EXPAND_WAVES
+#define GP_EXPAND_WAVES 0
+#endif
+#if GP_EXPAND_WAVES > 0
+#define EXPAND_BOUNDS __launch_bounds__(BLOCK, GP_EXPAND_WAVES)
+#else
+#define EXPAND_BOUNDS __launch_bounds__(BLOCK)
+#endif
 // rows each lane keeps in flight per gather step (MLP vs VGPRs)
 #ifndef GP_ROWS_IN_FLIGHT
 #define GP_ROWS_IN_FLIGHT 4
 #endif
 constexpr uint16_t SP_EMPTY = 0xFFFF;
 
+__device__ __forceinline__ bool is_list_row(uint32_t fp, int32_t list_max) {
+  return fp != 0u && fp <= (uint32_t)list_max;
+}
+
+// word `w` of row v (either format); for the rare paths (injection, push
+// staging, fixups, per-message sums) -- the gather has its own batched reader
+__device__ __forceinline__ u64 row_word(const u64* __restrict__ front, int64_t v, int words, uint32_t fp,
+                                        int32_t list_max, int w) {
+  if (fp == 0u) return 0ull;
+  if (is_list_row(fp, list_max)) {
+    const uint16_t* ids = reinterpret_cast<const uint16_t*>(front + (size_t)v * words);
+    u64 x = 0;
+#pragma unroll 4
+    for (int q = 0; q < LIST_SLOTS; ++q) {
+      const uint16_t id = ids[q];
+      if (id != SP_EMPTY && (int)(id >> 6) == w) x |= 1ull << (id & 63);
+    }
+    return x;
+  }
+  return front[(size_t)v * words + w];
+}
+
+// write the <= LIST_MAX ids staged in ids[0, tot) as the list segment of a row
+// slot: lanes 0..3 store 16 B (8 ids) each, 0xFFFF past tot
+__device__ __forceinline__ void store_list(u64* __restrict__ slot, const uint16_t* __restrict__ ids, uint32_t tot,
+                                           int lane) {
+  if (lane < 4) {
+    u64 p[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      u64 x = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t q = (uint32_t)(lane * 8 + h * 4 + k);
+        const u64 id = q < tot ? (u64)ids[q] : (u64)SP_EMPTY;
+        x |= id << (16 * k);
+      }
+      p[h] = x;
+    }
+    *reinterpret_cast<u64x2*>(slot + lane * 2) = u64x2{p[0], p[1]};
+  }
+}
+
+// per-wave LDS of the pull kernels
 struct WaveLds {
-  int32_t idx[64];      // dense-format active neighbours (tagged ids)
-  int32_t sidx[64];     // id-list-format active neighbours
   u64 acc[64];          // OR accumulator of id-list rows
   u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
-  uint16_t ids[64];     // id-list staging of finish_row
+  int32_t idx[64];      // bitmap-row active neighbours of one pass
+  int32_t sidx[64];     // id-list-row active neighbours of one pass
+  uint16_t ids[64];     // id-list staging (finish_row)
   uint32_t nids;        // id-list fill cursor
 };
 
@@ -269,52 +290,74 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
   }
 }
 
-// OR the frontier rows of the active in-neighbours in arcs [b, e) into acc.
-// Neighbour ids come 64 at a time from the gather-order CSR (in-lists sorted
-// by neighbour degree, hubs first), are filtered by the L2-resident activity
-// bitmap and staged in LDS compacted to the active ones; id-list rows are
-// folded through the LDS row first, dense rows then stream into registers.
-// Early exit (bottom-up, Beamer et al. SC'12): with `ee` the wave stops once
-// acc | seen covers every message of the vertex's component (cm) -- group-0
-// lanes hold the seen (sv) and mask (cm) pieces.  OR is idempotent, so
-// acc & ~seen is exactly what the full scan would give.
-template <int W>
-__device__ __forceinline__ void gather(const ExpandArgs& a, int64_t b, int64_t e, WaveLds& L,
-                                       int lane, int g, int lw, u64x2& acc, WaveStats& st, bool ee,
-                                       u64x2 want) {
+// scan modes of a pull round (compile-time, so each variant keeps only the
+// registers it needs): the per-arc activity probe, plus id-list rows, or no
+// probe at all (unfiltered dense rounds)
+enum ScanMode { SCAN_FILTERED = 0, SCAN_LISTS = 1, SCAN_UNFILTERED = 2 };
+
+// classify neighbour u for the round: u (bitmap row), -(u + 2) (id-list row),
+// -1 (inactive: its row is never read).  Split in two so the probe load can be
+// issued a vertex ahead of its use (k_expand's pipeline): probe_raw issues the
+// bitmap load, classify decodes it.
+template <int MODE>
+__device__ __forceinline__ u64x2 probe_raw(const ExpandArgs& a, int32_t u) {
+  if constexpr (MODE == SCAN_UNFILTERED) {   // dense round: no bitmap probe (it misses L2 under the row stream)
+    return u64x2{0, 0};
+  } else if constexpr (MODE == SCAN_LISTS) {  // one 16-byte probe: activity + list format
+    return a.bits2[u >> 6];
+  } else {
+    return u64x2{reinterpret_cast<const u64*>(a.bits2)[(u >> 6) * 2], 0};
+  }
+}
+template <int MODE>
+__device__ __forceinline__ int32_t classify(u64x2 pb, int32_t u) {
+  if constexpr (MODE == SCAN_UNFILTERED) {
+    return u;
+  } else {
+    if (!((pb.x >> (u & 63)) & 1ull)) return -1;
+    if constexpr (MODE == SCAN_LISTS) return ((pb.y >> (u & 63)) & 1ull) ? -(u + 2) : u;
+    return u;
+  }
+}
+template <int MODE>
+__device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
+  return classify<MODE>(probe_raw<MODE>(a, u), u);
+}
+
+// OR the staged rows of one pass into acc: id lists (L.sidx[0, scnt)) through
+// the LDS row, bitmap rows (L.idx[0, cnt)) into registers, GP_ROWS_IN_FLIGHT
+// wave-instructions of 16 B per lane in flight.  Early exit (bottom-up,
+// Beamer et al. SC'12): with `ee` the wave stops once acc | seen covers every
+// message of the vertex's component (want = cm & ~seen, group-0 lanes); OR is
+// idempotent, so acc & ~seen is exactly what the full scan would give.
+// Returns true on early exit.
+template <int W, bool LISTS>
+__device__ __forceinline__ bool gather_rows(const ExpandArgs& a, WaveLds& L, int cnt, int scnt, int lane, int g,
+                                            int lw, u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
   constexpr int RPI = Geo<W>::RPI;
   constexpr int WPL = Geo<W>::WPL;
-  const bool sparse_ok = (W >= 32) && a.ids != nullptr;
-  for (int64_t j0 = b; j0 < e; j0 += 64) {
-    const int n = (int)min((int64_t)64, e - j0);
-    int32_t tu = 0;   // column id, bit 31 = hub row (cache-steered)
-    bool act = false, spr = false;
-    if (lane < n) {
-      tu = a.steer ? __builtin_nontemporal_load(a.gcol + j0 + lane) : a.gcol[j0 + lane];
-      const int32_t u = tu & 0x7FFFFFFF;
-      if (a.unfiltered) {   // dense round: no bitmap probe (it misses L2 under the row stream)
-        act = true;
-      } else {
-        act = (a.abits[u >> 6] >> (u & 63)) & 1ull;
-        if (act && sparse_ok) spr = (a.sbits[u >> 6] >> (u & 63)) & 1ull;
-      }
-    }
-    const u64 dmask = __ballot(act && !spr);
-    const u64 smask = __ballot(spr);
-    const int cnt = __popcll(dmask), scnt = __popcll(smask);
-    st.add(S_ARCS, n);
-    if (cnt + scnt == 0) continue;
-    if (act && !spr) L.idx[lane_rank(dmask)] = tu;
-    if (spr) L.sidx[lane_rank(smask)] = tu & 0x7FFFFFFF;
+  if constexpr (LISTS && W >= 16) {
     if (scnt) {
       if (lane < W) L.acc[lane] = 0ull;
       wave_sync_lds();
-      for (int k0 = 0; k0 < scnt; k0 += 64 / SPK) {   // two id lists per wave-instruction
-        const int k = k0 + lane / SPK;
-        if (k < scnt) {
-          const int32_t u = L.sidx[k];
-          const uint16_t id = a.ids[(size_t)u * SPK + (lane % SPK)];
-          if (id != SP_EMPTY) atomicOr(&L.acc[id >> 6], 1ull << (id & 63));
+      // 8 lanes per 64-byte list (8 B = 4 ids each), 8 lists per
+      // wave-instruction, LQ instructions in flight before the first LDS OR
+      constexpr int LQ = 4;
+      for (int k0 = 0; k0 < scnt; k0 += 8 * LQ) {
+        u64 r[LQ];
+#pragma unroll
+        for (int q = 0; q < LQ; ++q) {
+          const int k = k0 + q * 8 + (lane >> 3);
+          r[q] = ~0ull;
+          if (k < scnt) r[q] = a.front[(size_t)L.sidx[k] * W + (lane & 7)];
+        }
+#pragma unroll
+        for (int q = 0; q < LQ; ++q) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t id = (uint32_t)(r[q] >> (16 * k)) & 0xFFFFu;
+            if (id != SP_EMPTY) atomicOr(&L.acc[id >> 6], 1ull << (id & 63));
+          }
         }
       }
       wave_sync_lds();
@@ -324,33 +367,73 @@ __device__ __forceinline__ void gather(const ExpandArgs& a, int64_t b, int64_t e
       }
       st.add(S_GATHERED, scnt);
       st.add(S_SP_GATHERED, scnt);
-    } else {
-      wave_sync_lds();
     }
-    bool stop = false;
-    for (int k0 = 0; k0 < cnt; k0 += GP_ROWS_IN_FLIGHT * RPI) {
-      const bool steer = a.steer != 0;
-      u64x2 r[GP_ROWS_IN_FLIGHT];
+  }
+  for (int k0 = 0; k0 < cnt; k0 += GP_ROWS_IN_FLIGHT * RPI) {
+    u64x2 r[GP_ROWS_IN_FLIGHT];
 #pragma unroll
-      for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
-        const int k = k0 + g + q * RPI;
-        r[q] = u64x2{0, 0};
-        if (k < cnt) r[q] = load_row<W>(a.front, L.idx[k], lw, steer);
-      }
-#pragma unroll
-      for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
-      st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
-      if (ee) {
-        u64x2 t = acc;
-        reduce_slots<W>(t);
-        u64x2 miss = {0, 0};
-        if (g == 0) miss = want & ~t;
-        if (!__any((miss.x | miss.y) != 0ull)) {
-          stop = true;
-          break;
-        }
-      }
+    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
+      const int k = k0 + g + q * RPI;
+      r[q] = u64x2{0, 0};
+      if (k < cnt) r[q] = load_piece<W>(a.front, L.idx[k], lw);
     }
+#pragma unroll
+    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
+    st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
+    if (ee) {
+      u64x2 t = acc;
+      reduce_slots<W>(t);
+      u64x2 miss = {0, 0};
+      if (g == 0) miss = want & ~t;
+      if (!__any((miss.x | miss.y) != 0ull)) return true;
+    }
+  }
+  return false;
+}
+
+// stage one pass of classified neighbours (e: this lane's entry) in LDS;
+// returns the counts through cnt / scnt
+__device__ __forceinline__ void stage_pass(WaveLds& L, int32_t e, int lane, int& cnt, int& scnt) {
+  const u64 dmask = __ballot(e >= 0);
+  const u64 smask = __ballot(e < -1);
+  cnt = __popcll(dmask);
+  scnt = __popcll(smask);
+  if (e >= 0) L.idx[lane_rank(dmask)] = e;
+  if (e < -1) L.sidx[lane_rank(smask)] = -(e + 2);
+  wave_sync_lds();
+}
+
+// early exit: park the receiver's seen row in LDS (finish_row reuses it) and
+// return, in group-0 lanes, the messages of its component it still lacks
+template <int W>
+__device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, int64_t i, WaveLds& L, int g,
+                                                   int lw) {
+  constexpr int WPL = Geo<W>::WPL;
+  u64x2 want = {0, 0};
+  if (g == 0) {
+    const u64x2 sv = load_piece<W>(a.seen, i, lw);
+    const u64x2 cm = load_piece<W>(a.cmask, a.midx[v], lw);
+    L.seen[lw * WPL] = sv.x;
+    if constexpr (WPL == 2) L.seen[lw * WPL + 1] = sv.y;
+    want = cm & ~sv;
+  }
+  return want;
+}
+
+// per-receiver scan of arcs [b, e): 64 arcs per pass -- column ids, activity
+// probes, staging, gather
+template <int W, int MODE>
+__device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int64_t e, WaveLds& L, int lane,
+                                            int g, int lw, u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
+  for (int64_t j0 = b; j0 < e; j0 += 64) {
+    const int n = (int)min((int64_t)64, e - j0);
+    int32_t ent = -1;
+    if (lane < n) ent = probe<MODE>(a, a.gcol[j0 + lane]);
+    st.add(S_ARCS, n);
+    int cnt, scnt;
+    stage_pass(L, ent, lane, cnt, scnt);
+    if (cnt + scnt == 0) continue;
+    const bool stop = gather_rows<W, MODE == SCAN_LISTS>(a, L, cnt, scnt, lane, g, lw, acc, st, ee, want);
     wave_sync_lds();
     if (stop) break;
   }
@@ -375,10 +458,11 @@ __device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int w
   }
 }
 
-// receiver side of vertex v (local index i): apply seen, write next, counters
+// receiver side of vertex v (local index i): apply seen, write next, counters.
+// have_sv: the seen row is parked in L.seen (early exit), else it is loaded here.
 template <int W>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
-                                           int g, int lw, WaveStats& st, WaveLds& L, bool have_sv = false) {
+                                           int g, int lw, WaveStats& st, WaveLds& L, bool have_sv) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
@@ -392,7 +476,7 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
       sv.x = L.seen[lw * WPL];
       if constexpr (WPL == 2) sv.y = L.seen[lw * WPL + 1];
     } else {
-      sv = a.steer ? load_piece_nt<W>(a.seen, i, lw) : load_piece<W>(a.seen, i, lw);
+      sv = load_piece<W>(a.seen, i, lw);
     }
     nw = acc & ~sv;
   }
@@ -402,8 +486,8 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
     if (lane == 0) a.fpop_next[v] = 0;
     return;
   }
-  const bool as_ids = (W >= 32) && a.ids_next != nullptr && tot <= (uint32_t)SPK;
-  if (as_ids) {   // compact the <= SPK new bits into a 64-byte id list (order is immaterial)
+  const bool as_ids = W >= 16 && tot <= (uint32_t)a.list_max;
+  if (as_ids) {   // compact the <= LIST_MAX new bits into a 64-byte id list (order is immaterial)
     if (lane == 0) L.nids = 0;
     wave_sync_lds();
     uint32_t off = 0;
@@ -425,21 +509,13 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
       }
     }
     wave_sync_lds();
-    if (lane < SPK) a.ids_next[(size_t)v * SPK + lane] = lane < (int)tot ? L.ids[lane] : SP_EMPTY;
+    store_list(a.next + (size_t)v * W, L.ids, tot, lane);
     wave_sync_lds();
-    if (lane == 0) a.fmt_next[v] = 1;
     st.add(S_SP_WRITTEN, 1);
-  } else if (a.fmt_next && lane == 0) {
-    a.fmt_next[v] = 0;
   }
   if (g == 0) {
-    if (a.steer) {
-      if (!as_ids) store_piece_nt<W>(a.next, v, lw, nw);
-      if (nw.x | nw.y) store_piece_nt<W>(a.seen, i, lw, sv | nw);
-    } else {
-      if (!as_ids) store_piece<W>(a.next, v, lw, nw);
-      if (nw.x | nw.y) store_piece<W>(a.seen, i, lw, sv | nw);
-    }
+    if (!as_ids) store_piece<W>(a.next, v, lw, nw);
+    if (nw.x | nw.y) store_piece<W>(a.seen, i, lw, sv | nw);
     if (a.first) {
       uint8_t* row = a.first + (size_t)i * (W * 64);
       if (nw.x) set_first_bytes(row, lw * WPL, nw.x, (uint32_t)a.rr);
@@ -465,23 +541,6 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   st.add(S_NEXT_ARCS, (u64)(uint32_t)max(a.deg_live[v], 0));
 }
 
-// early exit: park the receiver's seen row in LDS (finish_row reuses it) and
-// return, in group-0 lanes, the messages of its component it still lacks
-template <int W>
-__device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, int64_t i, WaveLds& L, int g,
-                                                   int lw) {
-  constexpr int WPL = Geo<W>::WPL;
-  u64x2 want = {0, 0};
-  if (g == 0) {
-    const u64x2 sv = a.steer ? load_piece_nt<W>(a.seen, i, lw) : load_piece<W>(a.seen, i, lw);
-    const u64x2 cm = load_piece<W>(a.cmask, a.midx[v], lw);
-    L.seen[lw * WPL] = sv.x;
-    if constexpr (WPL == 2) L.seen[lw * WPL + 1] = sv.y;
-    want = cm & ~sv;
-  }
-  return want;
-}
-
 __device__ __forceinline__ u64 wave_sum_u64(u64 x) {
 #pragma unroll
   for (int s = 32; s > 0; s >>= 1) x += __shfl_xor(x, s);
@@ -490,15 +549,17 @@ __device__ __forceinline__ u64 wave_sum_u64(u64 x) {
 
 // main pull kernel: a wave owns 64 consecutive vertices.  The per-vertex
 // checks (sender accounting, down / done / hub / no in-arcs) run lane-parallel
-// with coalesced loads; the wave then gathers, one vertex at a time, only for
-// the vertices that can still receive something.
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
+// with coalesced loads; the wave then scans, one receiver at a time, only the
+// vertices that can still receive something.  Kept lean on registers (72
+// VGPRs, 7 waves per SIMD): the dense rounds are bound by the rows in flight.
+template <int W, int MODE>
+__global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
   __shared__ WaveLds s_w[WAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
+  WaveLds& L = s_w[wib];
   WaveStats st;
   ws_zero(st);
   const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
@@ -518,6 +579,8 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
     }
     st.add(S_SENDS, wave_sum_u64(sends));
     st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
+    st.add(S_VISITED, (u64)__popcll(__ballot(need)));
+    const bool ee = a.early_exit != 0;
     u64 m = __ballot(need);
     while (m) {
       const int k = __ffsll((long long)m) - 1;
@@ -525,23 +588,21 @@ __global__ __launch_bounds__(BLOCK) void k_expand(ExpandArgs a) {
       const int64_t i = base + k;
       const int v = uniform((int)(a.vbegin + i));
       const int64_t vb = a.row_ptr[v], ve = a.row_ptr[v + 1];   // scalar loads
-      st.add(S_VISITED, 1);
-      const bool ee = a.early_exit != 0;
       u64x2 acc = {0, 0}, want = {0, 0};
       if (ee) {
         st.add(S_SEEN_READ, 1);
-        want = early_exit_target<W>(a, v, i, s_w[wib], g, lw);
+        want = early_exit_target<W>(a, v, i, L, g, lw);
       }
-      gather<W>(a, vb, ve, s_w[wib], lane, g, lw, acc, st, ee, want);
+      gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
-      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], ee);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, L, ee);
     }
   }
   flush_stats(st, a.partial);
 }
 
 // hubs, pass 1: one wave per (hub, arc chunk) -> partial OR row
-template <int W>
+template <int W, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
   __shared__ WaveLds s_w[WAVES];
@@ -559,7 +620,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
       const bool ee = a.early_exit != 0;
       u64x2 want = {0, 0};
       if (ee) want = early_exit_target<W>(a, h.v, i, s_w[wib], g, lw);
-      gather<W>(a, h.beg, h.end, s_w[wib], lane, g, lw, acc, st, ee, want);
+      gather_scan<W, MODE>(a, h.beg, h.end, s_w[wib], lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
     }
     const bool nz = __any((acc.x | acc.y) != 0);
@@ -593,7 +654,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
         for (int p = p0; p < p1; ++p)
           if (a.hub_pnz[p]) acc |= load_piece<W>(a.hub_partial, p, lw);
       }
-      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib]);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false);
     }
   }
   flush_stats(st, a.partial);
@@ -609,14 +670,14 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
 
 // active senders from the bitmap: one thread per 64-vertex word, block-level
 // compaction, one cursor add per block; big senders go to their own list
-__global__ __launch_bounds__(BLOCK) void k_active_list(const u64* __restrict__ abits, int64_t nwords,
+__global__ __launch_bounds__(BLOCK) void k_active_list(const u64x2* __restrict__ bits2, int64_t nwords,
                                                        const int64_t* __restrict__ orp, int32_t big_thr,
                                                        int32_t* __restrict__ active, int32_t* __restrict__ big,
                                                        u64* __restrict__ stats) {
   __shared__ uint32_t s_cnt[BLOCK];
   __shared__ u64 s_base;
   const int64_t w = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const u64 bits = w < nwords ? abits[w] : 0ull;
+  const u64 bits = w < nwords ? bits2[w].x : 0ull;
   s_cnt[threadIdx.x] = (uint32_t)__popcll(bits);
   __syncthreads();
   for (int o = 1; o < BLOCK; o <<= 1) {   // inclusive scan
@@ -700,11 +761,12 @@ template <int W>
 __device__ __forceinline__ int stage_row(const ExpandArgs& a, int32_t u, u64* __restrict__ srow,
                                          int8_t* __restrict__ swords, int lane) {
   u64 x = 0;
-  if (W >= 32 && a.ids && a.fmt[u]) {   // id-list row: rebuild the words through LDS
+  const uint32_t fp = a.fpop[u];
+  if (W >= 16 && is_list_row(fp, a.list_max)) {   // id-list row: rebuild the words through LDS
     if (lane < W) srow[lane] = 0ull;
     wave_sync_lds();
-    if (lane < SPK) {
-      const uint16_t id = a.ids[(size_t)u * SPK + lane];
+    if (lane < LIST_SLOTS) {
+      const uint16_t id = reinterpret_cast<const uint16_t*>(a.front + (size_t)u * W)[lane];
       if (id != SP_EMPTY) atomicOr(&srow[id >> 6], 1ull << (id & 63));
     }
     wave_sync_lds();
@@ -746,7 +808,7 @@ __global__ __launch_bounds__(BLOCK) void k_push(ExpandArgs a) {
     const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
     const int64_t jb = a.orp[u], je = a.orp[u + 1];
     st.add(S_GATHERED, 1);
-    if (W >= 32 && a.ids && a.fmt[u]) st.add(S_SP_GATHERED, 1);
+    if (W >= 16 && is_list_row(a.fpop[u], a.list_max)) st.add(S_SP_GATHERED, 1);
     st.add(S_ARCS, (u64)(je - jb));
     st.add(S_ATOMICS, (u64)(je - jb) * (u64)nnz);
     push_arcs<W>(a, jb, je, s_row[wib], s_words[wib], nnz, lane);
@@ -812,26 +874,23 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
       store_piece<W>(a.acc, v, lw, u64x2{0, 0});
     }
     st.add(S_VISITED, 1);
-    finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib]);
+    finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false);
   }
   flush_stats(st, a.partial);
 }
 
-// frontier activity bitmap: bit v of abits = (fpop[v] != 0); one wave per 64 vertices
-__global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop,
-                                                  const uint8_t* __restrict__ fmt, u64* __restrict__ abits,
-                                                  u64* __restrict__ sbits, int64_t n) {
+// frontier bitmaps, interleaved per 64 vertices so one 16-byte probe answers
+// both questions: .x bit = (fpop != 0), .y bit = id-list row (1 <= fpop <= list_max)
+__global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, int32_t list_max,
+                                                  u64x2* __restrict__ bits2, int64_t n) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
     const int64_t v = v0 + lane;
-    const bool on = v < n && fpop[v] != 0u;
-    const u64 m = __ballot(on);
-    const u64 sm = __ballot(on && fmt && fmt[v] != 0);
-    if (lane == 0) {
-      abits[v0 >> 6] = m;
-      sbits[v0 >> 6] = sm;
-    }
+    const uint32_t fp = v < n ? fpop[v] : 0u;
+    const u64 m = __ballot(fp != 0u);
+    const u64 sm = __ballot(is_list_row(fp, list_max));
+    if (lane == 0) bits2[v0 >> 6] = u64x2{m, sm};
   }
 }
 
@@ -840,29 +899,21 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
 // or crashed) become zero, id-list rows are expanded to bitmap rows.  One wave
 // per 64-vertex bitmap word; fully active dense words cost one load.
 template <int W>
-__global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64* __restrict__ abits, const u64* __restrict__ sbits,
-                                                      const uint16_t* __restrict__ ids, uint8_t* __restrict__ fmt,
+__global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64x2* __restrict__ bits2,
+                                                      const uint32_t* __restrict__ fpop, int32_t list_max,
                                                       u64* __restrict__ front, int64_t n_alloc) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
   if (w * 64 >= n_alloc) return;
-  const u64 sp = (ids != nullptr) ? sbits[w] : 0ull;
-  u64 todo = ~abits[w] | sp;
+  const u64x2 pb = bits2[w];
+  u64 todo = ~pb.x | pb.y;
   while (todo) {
     const int b = __ffsll((long long)todo) - 1;
     todo &= todo - 1;
     const int64_t v = w * 64 + b;
     if (v >= n_alloc) break;
-    u64 x = 0;
-    if ((sp >> b) & 1ull) {
-      if constexpr (W >= 32) {
-        for (int q = 0; q < SPK; ++q) {
-          const uint16_t id = ids[(size_t)v * SPK + q];
-          if (id != SP_EMPTY && (id >> 6) == lane) x |= 1ull << (id & 63);
-        }
-      }
-      if (lane == 0) fmt[v] = 0;
-    }
+    const u64 x = ((pb.y >> b) & 1ull) ? row_word(front, v, W, fpop[v], list_max, lane) : 0ull;
+    __builtin_amdgcn_wave_barrier();   // every lane has read the list before it is overwritten
     if (lane < W) front[(size_t)v * W + lane] = x;
   }
 }
@@ -930,8 +981,7 @@ __global__ void k_done_at(const int32_t* __restrict__ comp, const uint32_t* __re
 // replicated on every rank, so every rank applies every group; the owner of
 // the origin also updates its Message-List, first-receipt and counters.
 struct InjectArgs {
-  const uint16_t* __restrict__ ids;    // id lists of frontier_r (null: dense only)
-  uint8_t* __restrict__ fmt;
+  int32_t list_max;                    // id-list rows (0: none)
   const int32_t* __restrict__ origin;
   const u64* __restrict__ bits;
   const uint32_t* __restrict__ cnt;
@@ -962,27 +1012,30 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
     if (a.state[o] & ST_DOWN) {
       if (owned) st.add(S_LOST, a.cnt[gi]);
     } else {
+      __shared__ uint16_t s_ids[WAVES][LIST_SLOTS];
       const uint32_t fp = a.fpop[o];
-      const bool was_ids = fp && a.ids && a.fmt[o];
       u64 b = 0, f = 0;
       if (lane < a.words) {
         b = a.bits[gi * a.words + lane];
-        if (was_ids) {   // the row is an id list: rebuild its word for this lane
-          for (int q = 0; q < SPK; ++q) {
-            const uint16_t id = a.ids[(size_t)o * SPK + q];
-            if (id != SP_EMPTY && (id >> 6) == lane) f |= 1ull << (id & 63);
-          }
-        } else if (fp) {
-          f = a.front[(size_t)o * a.words + lane];
+        f = row_word(a.front, o, a.words, fp, a.list_max, lane) | b;
+      }
+      const uint32_t pc = (uint32_t)__popcll(f);
+      const uint32_t tot = wave_sum_u32(pc);
+      __builtin_amdgcn_wave_barrier();   // the old row is read before it is rewritten
+      if (a.words >= 16 && tot <= (uint32_t)a.list_max) {   // still small: id list
+        uint32_t off = wave_excl_scan_u32(pc, lane);
+        u64 x = f;
+        while (x) {
+          const int bb = __ffsll((long long)x) - 1;
+          x &= x - 1;
+          s_ids[wib][off++] = (uint16_t)(lane * 64 + bb);
         }
-        f |= b;
+        wave_sync_lds();
+        store_list(a.front + (size_t)o * a.words, s_ids[wib], tot, lane);
+      } else if (lane < a.words) {
         a.front[(size_t)o * a.words + lane] = f;
       }
-      const uint32_t tot = wave_sum_u32((uint32_t)__popcll(f));
-      if (lane == 0) {
-        a.fpop[o] = tot;
-        if (a.fmt) a.fmt[o] = 0;   // injected rows are dense
-      }
+      if (lane == 0) a.fpop[o] = tot;
       if (owned) {
         const int64_t i = o - a.vbegin;
         if (lane < a.words) {
@@ -1124,10 +1177,9 @@ __global__ __launch_bounds__(BLOCK) void k_detect(LiveArgs a) {
 // over rows [0, count).  Lane l holds word l % W of vertex slot l / W; each lane
 // keeps 64 register counters per output.
 struct BitsumArgs {
-  const uint16_t* __restrict__ ids;   // optional id-list rows [count][SPK] (with fmt)
-  const uint8_t* __restrict__ fmt;
   const u64* __restrict__ rows;       // [count][W]
-  const uint32_t* __restrict__ guard; // optional: row valid iff guard[i] != 0
+  const uint32_t* __restrict__ guard; // optional: frontier popcounts (row valid iff != 0; format)
+  int32_t list_max;                   // with guard: rows with guard <= list_max are id lists
   const int32_t* __restrict__ weight; // [count]
   u64* __restrict__ cnt;              // [W*64] or null
   u64* __restrict__ wsum;             // [W*64] or null
@@ -1156,16 +1208,8 @@ __global__ __launch_bounds__(BLOCK) void k_bitsum(BitsumArgs a) {
   const int64_t step = (int64_t)gridDim.x * WAVES * VPS;
   for (int64_t i = ((int64_t)blockIdx.x * WAVES + wib) * VPS + q; i < a.count; i += step) {
     u64 x = 0;
-    if (!a.guard || a.guard[i] != 0) {
-      if (a.fmt && a.fmt[i]) {
-        for (int q = 0; q < SPK; ++q) {
-          const uint16_t id = a.ids[i * SPK + q];
-          if (id != SP_EMPTY && (id >> 6) == w) x |= 1ull << (id & 63);
-        }
-      } else {
-        x = a.rows[i * W + w];
-      }
-    }
+    if (!a.guard) x = a.rows[i * W + w];
+    else x = row_word(a.rows, i, W, a.guard[i], a.list_max, w);
     const uint32_t wt = SUM ? (uint32_t)max(a.weight[i], 0) : 0u;
 #pragma unroll
     for (int b = 0; b < 64; ++b) {
@@ -1216,18 +1260,13 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.col = c->d_col;
   a.front = c->d_front[c->cur];
   a.fpop = c->d_fpop[c->cur];
-  a.abits = c->d_abits;
-  a.sbits = c->d_sbits;
-  a.ids = c->d_ids[c->cur];
-  a.fmt = c->d_fmt[c->cur];
-  a.ids_next = c->d_ids[c->cur ^ 1];
-  a.fmt_next = c->d_fmt[c->cur ^ 1];
+  a.bits2 = c->d_bits2;
+  a.list_max = c->list_max();
   a.done_at = c->d_done_at;
   a.gcol = c->d_gcol;
   a.midx = c->d_midx;
   a.cmask = c->d_cmask;
   a.early_exit = c->early_exit_now ? 1 : 0;
-  a.steer = c->cfg.hot_degree > 0 ? 1 : 0;
   a.next = c->d_front[c->cur ^ 1];
   a.fpop_next = c->d_fpop[c->cur ^ 1];
   a.seen = c->d_seen;
@@ -1262,7 +1301,7 @@ template <int W>
 static void launch_push_w(Ctx* c, ExpandArgs a) {
   hipStream_t s = c->stream;
   const int64_t nwords = (c->n_alloc + 63) / 64;
-  hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_abits, nwords,
+  hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_bits2, nwords,
                      a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats);
   hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, a);
@@ -1280,15 +1319,31 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   const int64_t per_block = (int64_t)WAVES * 64;
   if (a.unfiltered)
     hipLaunchKernelGGL(k_fixup_rows<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
-                       c->d_abits, c->d_sbits, a.ids, c->d_fmt[c->cur], c->d_front[c->cur], c->n_alloc);
+                       c->d_bits2, c->d_fpop[c->cur], a.list_max, c->d_front[c->cur], c->n_alloc);
+  // id-list rows can only be present if the last round or this round's
+  // injection wrote some
+  const int mode = a.unfiltered ? SCAN_UNFILTERED : (c->lists_live ? SCAN_LISTS : SCAN_FILTERED);
   (void)hipEventRecord(c->ev[4], c->stream);
-  if (a.nloc > 0)
-    hipLaunchKernelGGL(k_expand<W>, dim3(grid_for(a.nloc, per_block)), dim3(BLOCK), 0, c->stream, a);
+  if (a.nloc > 0) {
+    const dim3 grid(grid_for(a.nloc, per_block));
+    if (mode == SCAN_UNFILTERED)
+      hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+    else if (mode == SCAN_LISTS)
+      hipLaunchKernelGGL((k_expand<W, SCAN_LISTS>), grid, dim3(BLOCK), 0, c->stream, a);
+    else
+      hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+  }
   (void)hipEventRecord(c->ev[5], c->stream);
   if (c->n_hub_items > 0) {
     ExpandArgs h = a;
     h.n_items = c->n_hub_items;
-    hipLaunchKernelGGL(k_hub_partial<W>, dim3(grid_for(h.n_items, WAVES)), dim3(BLOCK), 0, c->stream, h);
+    const dim3 grid(grid_for(h.n_items, WAVES));
+    if (mode == SCAN_UNFILTERED)
+      hipLaunchKernelGGL((k_hub_partial<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, h);
+    else if (mode == SCAN_LISTS)
+      hipLaunchKernelGGL((k_hub_partial<W, SCAN_LISTS>), grid, dim3(BLOCK), 0, c->stream, h);
+    else
+      hipLaunchKernelGGL((k_hub_partial<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, h);
     h.n_items = c->n_hubs;
     hipLaunchKernelGGL(k_hub_final<W>, dim3(grid_for(h.n_items, WAVES)), dim3(BLOCK), 0, c->stream, h);
   }
@@ -1296,8 +1351,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 
 static int launch_expand(Ctx* c) {
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
-                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_ids[0] ? c->d_fmt[c->cur] : nullptr,
-                     c->d_abits, c->d_sbits, c->n_alloc);
+                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->list_max(), c->d_bits2, c->n_alloc);
   // direction: push when the senders' arcs are a small share of all arcs
   const int r = c->round;
   // early exit pays once frontier rows are dense: >= m/16 new bits per vertex last round
@@ -1312,6 +1366,7 @@ static int launch_expand(Ctx* c) {
   const double senders = (double)c->prev_receivers + (double)c->inj_groups_at(r);
   c->unfiltered_now = !c->mode_push && c->cfg.unfiltered_pct > 0 &&
                       senders * 100.0 >= (double)c->cfg.unfiltered_pct * (double)c->n;
+  c->lists_live = c->list_max() > 0 && (c->prev_sp_written > 0 || c->inj_groups_at(r) > 0);
   ExpandArgs a{};
   fill_expand(c, a);
   a.unfiltered = c->unfiltered_now ? 1 : 0;
@@ -1405,9 +1460,7 @@ static void free_state(Ctx* c) {
   }
   dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_done_at);
-  dfree(&c->d_sbits);
-  for (int k = 0; k < 2; ++k) { dfree(&c->d_ids[k]); dfree(&c->d_fmt[k]); }
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_bits2); dfree(&c->d_done_at);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
@@ -1458,24 +1511,13 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_miss, na));
   GP_TRY(dalloc(&c->d_deg_live, na));
   GP_TRY(dalloc(&c->d_cand, na));
-  GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
-  GP_TRY(dalloc(&c->d_sbits, (na + 63) / 64));
-  for (int k = 0; k < 2; ++k) {
-    if (W >= 32 && c->cfg.sparse_rows) {
-      GP_TRY(dalloc(&c->d_ids[k], na * SPK));
-      GP_TRY(dalloc(&c->d_fmt[k], na));
-      GP_HIP(hipMemset(c->d_fmt[k], 0, na));
-    } else {
-      dfree(&c->d_ids[k]);
-      dfree(&c->d_fmt[k]);
-    }
-  }
+  GP_TRY(dalloc(&c->d_bits2, (na + 63) / 64));
   GP_TRY(dalloc(&c->d_done_at, na));
   c->done_at_valid = false;
   GP_TRY(dalloc(&c->d_acc, na * W));
-  GP_HIP(hipMemset(c->d_acc, 0, na * W * 8));
+  GP_HIP(hipMemsetAsync(c->d_acc, 0, na * W * 8, c->stream));
   GP_TRY(dalloc(&c->d_tbits, (na + 63) / 64));
-  GP_HIP(hipMemset(c->d_tbits, 0, (na + 63) / 64 * 8));
+  GP_HIP(hipMemsetAsync(c->d_tbits, 0, (na + 63) / 64 * 8, c->stream));
   GP_TRY(dalloc(&c->d_touched, na));
   GP_TRY(dalloc(&c->d_active, na));
   GP_TRY(dalloc(&c->d_big, na));
@@ -1484,6 +1526,7 @@ static int alloc_state(Ctx* c) {
   c->report_cap = std::max<int64_t>(c->cfg.report_capacity, 1);
   GP_TRY(dalloc(&c->d_reports, (size_t)c->report_cap));
   GP_TRY(dalloc(&c->d_hub_partial, std::max<size_t>(c->h_hub_items.size(), 1) * W));
+  GP_HIP(hipStreamSynchronize(c->stream));
   return 0;
 }
 
@@ -1533,7 +1576,9 @@ static int compute_done_at(Ctx* c, int64_t groups) {
   GP_TRY(dalloc(&ior, (size_t)c->n));
   GP_HIP(hipMemcpy(ior, idx_of_root.data(), (size_t)c->n * 4, hipMemcpyHostToDevice));
   GP_TRY(dalloc(&c->d_midx, (size_t)c->n_alloc));
-  GP_HIP(hipMemset(c->d_midx, 0xFF, (size_t)c->n_alloc * 4));
+  // on the engine stream: the stream is non-blocking, so a null-stream memset
+  // could land after k_midx
+  GP_HIP(hipMemsetAsync(c->d_midx, 0xFF, (size_t)c->n_alloc * 4, s));
   hipLaunchKernelGGL(k_midx, dim3(grid_for(c->n, 256)), dim3(256), 0, s, c->d_comp, ior, c->d_midx, c->n);
   GP_HIP(hipGetLastError());
   GP_HIP(hipStreamSynchronize(s));
@@ -1577,7 +1622,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->report_capacity = 1 << 20;
   cfg->push_ratio = 40.0;   // push when sender arcs <= nnz / 40
   cfg->early_exit = 1;
-  cfg->hot_degree = 0;
+  cfg->reserved0 = 0;
   cfg->sparse_rows = 0;
   cfg->unfiltered_pct = 90;
 }
@@ -1603,7 +1648,8 @@ int gp_create(int device, gp_ctx** out) {
     gp_destroy(c);
     return GP_ENOMEM;
   }
-  (void)hipMemset(c->d_stats, 0, (64 + (size_t)NPART * NST) * sizeof(u64));
+  (void)hipMemsetAsync(c->d_stats, 0, (64 + (size_t)NPART * NST) * sizeof(u64), c->stream);
+  (void)hipStreamSynchronize(c->stream);
   (void)hipHostMalloc((void**)&c->h_stats, 64 * sizeof(u64), hipHostMallocDefault);
   *out = c;
   return 0;
@@ -1615,9 +1661,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_done_at);
-  dfree(&c->d_sbits);
-  for (int k = 0; k < 2; ++k) { dfree(&c->d_ids[k]); dfree(&c->d_fmt[k]); }
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_bits2); dfree(&c->d_done_at);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -1641,10 +1685,8 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
   GP_HIP(hipSetDevice(c->device));
   const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
-  const bool hot_changed = cfg->hot_degree != c->cfg.hot_degree;
   c->cfg = *cfg;
   if (c->n > 0 && hub_changed) GP_TRY(build_hubs(c));
-  if (c->n > 0 && hot_changed) GP_TRY(build_gather_order(c));
   if (state_ready(c)) GP_TRY(alloc_state(c));
   return 0;
 }
@@ -1828,6 +1870,7 @@ int gp_reset(gp_ctx* c) {
   c->prev_next_arcs = 0;
   c->prev_new_bits = 0;
   c->prev_receivers = 0;
+  c->prev_sp_written = 0;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
   GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToDevice, s));
@@ -1848,6 +1891,7 @@ int gp_crash(gp_ctx* c, int32_t nverts, const int32_t* verts) {
   if (!state_ready(c)) return set_error(GP_ESTATE, "gp_reset first");
   GP_HIP(hipSetDevice(c->device));
   std::vector<uint8_t> st((size_t)c->n);
+  GP_HIP(hipStreamSynchronize(c->stream));
   GP_HIP(hipMemcpy(st.data(), c->d_state, (size_t)c->n, hipMemcpyDeviceToHost));
   for (int32_t k = 0; k < nverts; ++k) {
     if (verts[k] < 0 || verts[k] >= c->n) return set_error(GP_EINVAL, "vertex out of range");
@@ -1915,8 +1959,7 @@ static int round_launch(Ctx* c) {
     ia.cnt = c->d_inj_cnt;
     ia.front = c->d_front[c->cur];
     ia.fpop = c->d_fpop[c->cur];
-    ia.ids = c->d_ids[c->cur];
-    ia.fmt = c->d_ids[0] ? c->d_fmt[c->cur] : nullptr;
+    ia.list_max = c->list_max();
     ia.seen = c->d_seen;
     ia.seenpop = c->d_seenpop;
     ia.first = c->cfg.track_first ? c->d_first : nullptr;
@@ -1937,8 +1980,7 @@ static int round_launch(Ctx* c) {
     BitsumArgs b{};
     b.rows = c->d_front[c->cur] + (size_t)c->vbegin * c->words;
     b.guard = c->d_fpop[c->cur] + c->vbegin;
-    b.ids = c->d_ids[0] ? c->d_ids[c->cur] + (size_t)c->vbegin * SPK : nullptr;
-    b.fmt = c->d_ids[0] ? c->d_fmt[c->cur] + c->vbegin : nullptr;
+    b.list_max = c->list_max();
     b.weight = c->d_deg_live + c->vbegin;
     b.cnt = nullptr;
     b.wsum = c->d_msg_fwd;
@@ -1966,12 +2008,6 @@ static int round_exchange_rccl(Ctx* c) {
                         (size_t)c->slice * W, ncclUint64, c->comm, s));
   GP_RCCL(ncclAllGather(c->d_fpop[nx] + (size_t)c->rank * c->slice, c->d_fpop[nx],
                         (size_t)c->slice, ncclUint32, c->comm, s));
-  if (c->d_ids[0]) {
-    GP_RCCL(ncclAllGather(c->d_ids[nx] + (size_t)c->rank * c->slice * SPK, c->d_ids[nx],
-                          (size_t)c->slice * SPK * 2, ncclUint8, c->comm, s));
-    GP_RCCL(ncclAllGather(c->d_fmt[nx] + (size_t)c->rank * c->slice, c->d_fmt[nx], (size_t)c->slice,
-                          ncclUint8, c->comm, s));
-  }
   // the report cursor (slot S_REPORT_CURSOR) stays rank-local
   GP_RCCL(ncclAllReduce(c->d_stats, c->d_stats, S_REPORT_CURSOR, ncclUint64, ncclSum, c->comm, s));
   GP_RCCL(ncclGroupEnd());
@@ -2028,6 +2064,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   c->prev_next_arcs = h[S_NEXT_ARCS];
   c->prev_new_bits = h[S_NEW_BITS];
   c->prev_receivers = h[S_RECEIVERS];
+  c->prev_sp_written = h[S_SP_WRITTEN];
   c->cur ^= 1;
   c->round = r + 1;
   return 0;
@@ -2074,12 +2111,6 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
                             (size_t)(e - b) * W * 8, hipMemcpyDefault, dst->stream));
       GP_HIP(hipMemcpyAsync(dst->d_fpop[nx] + b, src->d_fpop[src->cur ^ 1] + b, (size_t)(e - b) * 4,
                             hipMemcpyDefault, dst->stream));
-      if (dst->d_ids[0] && src->d_ids[0]) {
-        GP_HIP(hipMemcpyAsync(dst->d_ids[nx] + (size_t)b * SPK, src->d_ids[src->cur ^ 1] + (size_t)b * SPK,
-                              (size_t)(e - b) * SPK * 2, hipMemcpyDefault, dst->stream));
-        GP_HIP(hipMemcpyAsync(dst->d_fmt[nx] + b, src->d_fmt[src->cur ^ 1] + b, (size_t)(e - b),
-                              hipMemcpyDefault, dst->stream));
-      }
     }
   }
   gp_round_stats sum;
@@ -2231,23 +2262,16 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       GP_HIP(hipMemcpy(fp.data(), c->d_fpop[c->cur], (size_t)n * 4, hipMemcpyDeviceToHost));
       GP_HIP(hipMemcpy(host, c->d_front[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
       uint64_t* h = static_cast<uint64_t*>(host);
-      std::vector<uint8_t> fm;
-      std::vector<uint16_t> ids;
-      if (c->d_ids[0]) {
-        fm.resize((size_t)n);
-        ids.resize((size_t)n * SPK);
-        GP_HIP(hipMemcpy(fm.data(), c->d_fmt[c->cur], (size_t)n, hipMemcpyDeviceToHost));
-        GP_HIP(hipMemcpy(ids.data(), c->d_ids[c->cur], (size_t)n * SPK * 2, hipMemcpyDeviceToHost));
-      }
+      const uint32_t lmax = (uint32_t)c->list_max();
       for (int64_t v = 0; v < n; ++v) {
         if (!fp[v]) {
           std::memset(h + v * W, 0, (size_t)W * 8);
-        } else if (!fm.empty() && fm[(size_t)v]) {
+        } else if (fp[v] <= lmax) {   // id-list row
+          uint16_t ids[LIST_SLOTS];
+          std::memcpy(ids, h + v * W, sizeof(ids));
           std::memset(h + v * W, 0, (size_t)W * 8);
-          for (int q = 0; q < SPK; ++q) {
-            const uint16_t id = ids[(size_t)v * SPK + q];
-            if (id != SP_EMPTY) h[v * W + (id >> 6)] |= 1ull << (id & 63);
-          }
+          for (int q = 0; q < LIST_SLOTS; ++q)
+            if (ids[q] != SP_EMPTY) h[v * W + (ids[q] >> 6)] |= 1ull << (ids[q] & 63);
         }
       }
       return 0;

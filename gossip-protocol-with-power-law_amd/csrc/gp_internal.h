@@ -26,6 +26,10 @@ enum StatSlot {
   S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR
 };
 
+// id-list frontier rows hold at most this many message ids (one 64-byte segment
+// of 32 u16 slots, 0xFFFF-padded)
+constexpr int LIST_MAX = 31;
+
 struct HubItem {       // one wave's share of a hub's in-list
   int32_t v;           // hub vertex
   int32_t hub;         // index into the hub table
@@ -79,10 +83,8 @@ struct Ctx {
   uint8_t* d_miss = nullptr;        // [n_alloc]
   int32_t* d_deg_live = nullptr;    // [n_alloc]
   int32_t* d_cand = nullptr;        // [n] detection candidates of a round
-  u64* d_abits = nullptr;           // [n_alloc/64] frontier activity bitmap
-  u64* d_sbits = nullptr;           // [n_alloc/64] frontier rows held as id lists
-  uint16_t* d_ids[2] = {nullptr, nullptr};   // [n_alloc][32] id-list rows (W >= 32 only)
-  uint8_t* d_fmt[2] = {nullptr, nullptr};    // [n_alloc] 1 = id-list row
+  // [n_alloc/64] per 64 vertices {active bits, id-list-row bits} of frontier_r
+  u64 __attribute__((ext_vector_type(2)))* d_bits2 = nullptr;
   // push (sparse-round) mode
   u64* d_acc = nullptr;             // [n_alloc][W] OR accumulator, kept all-zero between uses
   u64* d_tbits = nullptr;           // [n_alloc/64] receivers pushed to this round
@@ -96,6 +98,8 @@ struct Ctx {
   u64 prev_new_bits = 0;            // new bits of the last round (global)
   u64 prev_receivers = 0;           // receivers of the last round (global)
   bool unfiltered_now = false;      // this round's pull skips the activity check
+  u64 prev_sp_written = 0;          // id-list rows written by the last round (global)
+  bool lists_live = false;          // frontier_r may hold id-list rows
   int64_t inj_groups_at(int32_t r) const {
     auto it = inject.find(r);
     return it == inject.end() ? 0 : it->second.cnt;
@@ -135,6 +139,8 @@ struct Ctx {
   int cu_count = 256;
 
   int64_t nloc() const { return vend - vbegin; }
+  // frontier rows with at most this many bits are id lists
+  int32_t list_max() const { return (cfg.sparse_rows && words >= 16) ? LIST_MAX : 0; }
 };
 
 // error helpers (thread-local message, negative status)

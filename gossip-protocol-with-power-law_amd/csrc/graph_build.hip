@@ -202,17 +202,15 @@ int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed) 
 // gather order: each in-list re-sorted by the neighbour's in-degree, largest
 // first (stable: ties keep ascending ids).  Hubs hold most messages earliest,
 // so the early-exit pull covers a vertex's missing set after fewer rows.
-// bit 31 of a gather-order column tags a hub row (in-degree >= hot): the pull
-// loads it with the default (cacheable) policy and everything else non-temporal
 __global__ void k_gorder_keys(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
-                              u64* __restrict__ keys, int32_t* __restrict__ vals, int64_t n, int64_t hot) {
+                              u64* __restrict__ keys, int32_t* __restrict__ vals, int64_t n) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= n) return;
   for (int64_t j = rp[v]; j < rp[v + 1]; ++j) {
     const int32_t u = col[j];
     const uint32_t d = (uint32_t)(rp[u + 1] - rp[u]);
     keys[j] = ((u64)v << 32) | (u64)(0xFFFFFFFFu - d);
-    vals[j] = (hot > 0 && (int64_t)d >= hot) ? (int32_t)((uint32_t)u | 0x80000000u) : u;
+    vals[j] = u;
   }
 }
 
@@ -226,7 +224,7 @@ int build_gather_order(Ctx* c) {
   GP_HIP(hipMalloc(&kb.p, (size_t)A * 8));
   GP_HIP(hipMalloc(&va.p, (size_t)A * 4));
   hipLaunchKernelGGL(k_gorder_keys, dim3((unsigned)((c->n + 255) / 256)), dim3(256), 0, s, c->d_row_ptr,
-                     c->d_col, (u64*)ka.p, (int32_t*)va.p, c->n, (int64_t)c->cfg.hot_degree);
+                     c->d_col, (u64*)ka.p, (int32_t*)va.p, c->n);
   GP_HIP(hipGetLastError());
   size_t tb = 0;
   GP_HIP(rocprim::radix_sort_pairs(nullptr, tb, (u64*)ka.p, (u64*)kb.p, (int32_t*)va.p, c->d_gcol, (size_t)A,

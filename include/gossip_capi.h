@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 2
+#define GP_ABI_VERSION 3
 
 typedef struct gp_ctx gp_ctx;
 
@@ -102,9 +102,9 @@ typedef struct gp_config {
   double push_ratio;           /* push a round when its sender arcs * push_ratio <= nnz;
                                   0 = always pull                      */
   int32_t early_exit;          /* coverage-checked pull scans in dense rounds (§3.4)   */
-  int32_t hot_degree;          /* > 0: rows of vertices with in-degree >= hot_degree are
-                                  loaded cacheable, all other streams non-temporal (§3.5) */
-  int32_t sparse_rows;         /* W >= 32: rows with <= 32 new bits stored as id lists */
+  int32_t reserved0;           /* must be 0 (was a cache-steering knob; measured no effect) */
+  int32_t sparse_rows;         /* W >= 16: frontier rows with <= 31 bits are stored as
+                                  64-byte id lists in their row slot   */
   int32_t unfiltered_pct;      /* pull without the per-arc activity check when >= this %
                                   of vertices are senders (0 = never)   */
 } gp_config;

@@ -1,0 +1,15 @@
+#!/bin/bash
+# build an experimental libgossip_hip.so variant: build_variant.sh NAME "-DFLAG=..."
+# output: gossip-protocol-with-power-law_amd/_variants/NAME.so (git-ignored)
+set -e
+cd "$(dirname "$0")/.."
+PKG=gossip-protocol-with-power-law_amd
+OUT=$PKG/_variants/$1
+mkdir -p $OUT
+F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 $2"
+/opt/rocm/bin/hipcc $F -c $PKG/csrc/gossip_engine.hip -o $OUT/ge.o &
+/opt/rocm/bin/hipcc $F -c $PKG/csrc/graph_build.hip -o $OUT/gb.o &
+wait
+/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o -o $PKG/_variants/$1.so -lrccl
+rm -rf $OUT
+echo $PKG/_variants/$1.so

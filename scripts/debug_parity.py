@@ -11,6 +11,7 @@ push = float(sys.argv[1]) if len(sys.argv) > 1 else 0.0
 sparse = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 ee = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 churn = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+unf = int(sys.argv[5]) if len(sys.argv) > 5 else 0
 rp, col = oracle.chung_lu(60_000, 10, 2.4, 21)
 g = pkg.CSR(60_000, rp, col, False)
 m = 4096
@@ -20,7 +21,7 @@ kw = dict(churn=True, p_fail=0.01, churn_seed=5) if churn else {}
 ref = oracle.run(g, origin, inject, want_first=True, **kw)
 eng = pkg.GossipEngine(0, track_first=1, track_digest=1, churn=churn, p_fail=0.01 if churn else 0.0,
                        churn_seed=5, hub_threshold=512, push_ratio=push, sparse_rows=sparse,
-                       early_exit=ee, track_msg_forwards=churn)
+                       early_exit=ee, track_msg_forwards=churn, unfiltered_pct=unf)
 eng.load_graph(g)
 eng.set_messages(origin, inject)
 eng.reset()
