@@ -405,13 +405,15 @@ __device__ __forceinline__ void stage_pass(WaveLds& L, int32_t e, int lane, int&
 
 // early exit: park the receiver's seen row in LDS (finish_row reuses it) and
 // return, in group-0 lanes, the messages of its component it still lacks
+// (spop == 0: the row was never written this run and reads as zero -- reset
+// does not clear the Message-Lists)
 template <int W>
 __device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, int64_t i, WaveLds& L, int g,
-                                                   int lw) {
+                                                   int lw, uint32_t spop) {
   constexpr int WPL = Geo<W>::WPL;
   u64x2 want = {0, 0};
   if (g == 0) {
-    const u64x2 sv = load_piece<W>(a.seen, i, lw);
+    const u64x2 sv = spop ? load_piece<W>(a.seen, i, lw) : u64x2{0, 0};
     const u64x2 cm = load_piece<W>(a.cmask, a.midx[v], lw);
     L.seen[lw * WPL] = sv.x;
     if constexpr (WPL == 2) L.seen[lw * WPL + 1] = sv.y;
@@ -459,23 +461,25 @@ __device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int w
 }
 
 // receiver side of vertex v (local index i): apply seen, write next, counters.
-// have_sv: the seen row is parked in L.seen (early exit), else it is loaded here.
+// have_sv: the seen row is parked in L.seen (early exit), else it is loaded
+// here -- unless spop (|seen(v)|) is 0: a row never written this run reads as
+// zero (reset does not clear the Message-Lists).
 template <int W>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
-                                           int g, int lw, WaveStats& st, WaveLds& L, bool have_sv) {
+                                           int g, int lw, WaveStats& st, WaveLds& L, bool have_sv, uint32_t spop) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
     if (lane == 0) a.fpop_next[v] = 0;
     return;
   }
-  if (!have_sv) st.add(S_SEEN_READ, 1);
+  if (!have_sv && spop) st.add(S_SEEN_READ, 1);
   u64x2 sv = {0, 0}, nw = {0, 0};
   if (g == 0) {
     if (have_sv) {
       sv.x = L.seen[lw * WPL];
       if constexpr (WPL == 2) sv.y = L.seen[lw * WPL + 1];
-    } else {
+    } else if (spop) {
       sv = load_piece<W>(a.seen, i, lw);
     }
     nw = acc & ~sv;
@@ -515,7 +519,8 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   }
   if (g == 0) {
     if (!as_ids) store_piece<W>(a.next, v, lw, nw);
-    if (nw.x | nw.y) store_piece<W>(a.seen, i, lw, sv | nw);
+    // a row first written this run is written whole (its stale pieces go)
+    if ((nw.x | nw.y) || spop == 0) store_piece<W>(a.seen, i, lw, sv | nw);
     if (a.first) {
       uint8_t* row = a.first + (size_t)i * (W * 64);
       if (nw.x) set_first_bytes(row, lw * WPL, nw.x, (uint32_t)a.rr);
@@ -567,6 +572,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     const int64_t li = base + lane;
     bool need = false, act = false;
     u64 sends = 0;
+    uint32_t sp = 0;
     if (li < a.nloc) {
       const int v = (int)(a.vbegin + li);
       const uint32_t fp = a.fpop[v];
@@ -574,7 +580,8 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
       const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
-      need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
+      sp = a.seenpop[li];
+      need = !(a.state[v] & ST_DOWN) && sp < a.done_at[v] && !hub && e > b;
       if (!need && !hub) a.fpop_next[v] = 0;
     }
     st.add(S_SENDS, wave_sum_u64(sends));
@@ -588,14 +595,15 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       const int64_t i = base + k;
       const int v = uniform((int)(a.vbegin + i));
       const int64_t vb = a.row_ptr[v], ve = a.row_ptr[v + 1];   // scalar loads
+      const uint32_t spop = (uint32_t)__builtin_amdgcn_readlane((int)sp, k);
       u64x2 acc = {0, 0}, want = {0, 0};
       if (ee) {
-        st.add(S_SEEN_READ, 1);
-        want = early_exit_target<W>(a, v, i, L, g, lw);
+        if (spop) st.add(S_SEEN_READ, 1);
+        want = early_exit_target<W>(a, v, i, L, g, lw, spop);
       }
       gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
-      finish_row<W>(a, v, i, acc, lane, g, lw, st, L, ee);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, L, ee, spop);
     }
   }
   flush_stats(st, a.partial);
@@ -616,10 +624,11 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
     const HubItem h = a.hub_items[it];
     const int64_t i = h.v - a.vbegin;
     u64x2 acc = {0, 0};
-    if (!(a.state[h.v] & ST_DOWN) && a.seenpop[i] < a.done_at[h.v]) {
+    const uint32_t spop = a.seenpop[i];
+    if (!(a.state[h.v] & ST_DOWN) && spop < a.done_at[h.v]) {
       const bool ee = a.early_exit != 0;
       u64x2 want = {0, 0};
-      if (ee) want = early_exit_target<W>(a, h.v, i, s_w[wib], g, lw);
+      if (ee) want = early_exit_target<W>(a, h.v, i, s_w[wib], g, lw, spop);
       gather_scan<W, MODE>(a, h.beg, h.end, s_w[wib], lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
     }
@@ -644,7 +653,8 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
   if (h < a.n_items) {
     const int v = a.hubs[h];
     const int64_t i = v - a.vbegin;
-    if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= a.done_at[v]) {
+    const uint32_t spop = a.seenpop[i];
+    if ((a.state[v] & ST_DOWN) || spop >= a.done_at[v]) {
       if (lane == 0) a.fpop_next[v] = 0;
     } else {
       st.add(S_VISITED, 1);
@@ -654,7 +664,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
         for (int p = p0; p < p1; ++p)
           if (a.hub_pnz[p]) acc |= load_piece<W>(a.hub_partial, p, lw);
       }
-      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, spop);
     }
   }
   flush_stats(st, a.partial);
@@ -874,7 +884,7 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
       store_piece<W>(a.acc, v, lw, u64x2{0, 0});
     }
     st.add(S_VISITED, 1);
-    finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false);
+    finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.seenpop[i]);
   }
   flush_stats(st, a.partial);
 }
@@ -1038,8 +1048,9 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
       if (lane == 0) a.fpop[o] = tot;
       if (owned) {
         const int64_t i = o - a.vbegin;
+        const uint32_t sp0 = a.seenpop[i];   // 0: the row is stale from an earlier run
         if (lane < a.words) {
-          a.seen[i * a.words + lane] |= b;
+          a.seen[i * a.words + lane] = (sp0 ? a.seen[i * a.words + lane] : 0ull) | b;
           if (a.first && b) set_first_bytes(a.first + (size_t)i * a.words * 64, lane, b, (uint32_t)a.r);
         }
         const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
@@ -1859,7 +1870,6 @@ int gp_reset(gp_ctx* c) {
   }
   const size_t W = (size_t)c->words, na = (size_t)c->n_alloc, nl = (size_t)std::max<int64_t>(c->nloc(), 1);
   hipStream_t s = c->stream;
-  GP_HIP(hipMemsetAsync(c->d_seen, 0, nl * W * 8, s));
   GP_HIP(hipMemsetAsync(c->d_seenpop, 0, nl * 4, s));
   GP_HIP(hipMemsetAsync(c->d_fpop[0], 0, na * 4, s));
   GP_HIP(hipMemsetAsync(c->d_fpop[1], 0, na * 4, s));
@@ -2169,7 +2179,8 @@ int gp_finalize_messages(gp_ctx* c) {
   if (fwd_from_seen) GP_HIP(hipMemsetAsync(fwd_local, 0, M * 8, s));
   BitsumArgs b{};
   b.rows = c->d_seen;
-  b.guard = nullptr;
+  b.guard = c->d_seenpop;   // rows with |seen| == 0 are stale (reset does not clear them)
+  b.list_max = 0;
   b.weight = c->d_deg_out + c->vbegin;
   b.cnt = cov;
   b.wsum = fwd_from_seen ? fwd_local : nullptr;
@@ -2202,7 +2213,14 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
     case GP_SEEN:
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(nl * W * 8));
-      if (bytes) GP_HIP(hipMemcpy(host, c->d_seen, (size_t)bytes, hipMemcpyDeviceToHost));
+      if (bytes) {
+        GP_HIP(hipMemcpy(host, c->d_seen, (size_t)bytes, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> sp((size_t)nl);
+        GP_HIP(hipMemcpy(sp.data(), c->d_seenpop, (size_t)nl * 4, hipMemcpyDeviceToHost));
+        uint64_t* h = static_cast<uint64_t*>(host);
+        for (int64_t v = 0; v < nl; ++v)   // rows never written this run are stale
+          if (!sp[(size_t)v]) std::memset(h + v * W, 0, (size_t)W * 8);
+      }
       return 0;
     case GP_FIRST:
       if (!run) return set_error(GP_ESTATE, "no run state");
