@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-messages", type=int, default=64)
+    ap.add_argument("--parallel", choices=("messages", "vertex"), default="messages",
+                    help="N > 1: message shards (no data-path collective, default) or the vertex "
+                         "partition with an RCCL all-gather of the next rows every round")
     ap.add_argument("--profile-steps", action="store_true",
                     help="print per-round stats of the last step to stderr")
     return ap.parse_args()
@@ -100,18 +103,25 @@ def main():
     world, rank, local = dist.env()
     pg = dist.init("gloo")
     n = 1 << args.log2n
-    eng = pkg.GossipEngine(local, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
+    # one GPU per rank; on a smaller box (rehearsal) ranks share devices round-robin
+    device = local % max(pkg._lib.device_count(), 1)
+    eng = pkg.GossipEngine(device, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
                            push_ratio=args.push_ratio,
                            early_exit=args.early_exit, sparse_rows=args.sparse_rows,
                            unfiltered_pct=args.unfiltered_pct)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()
-    if world > 1:
+    shards = world > 1 and args.parallel == "messages"
+    if world > 1 and not shards:
         eng.set_partition(rank, world)
         eng.comm_init(dist.share_comm_id(pg, pkg.GossipEngine.comm_unique_id), world, rank)
     origin = pkg.overlay.random_origins(n, args.messages, seed=args.seed)
-    eng.set_messages(origin)
+    if shards:   # this rank's word-aligned block of the 4096 messages
+        lo, hi = dist.message_shard(args.messages, world, rank)
+        eng.set_message_shard(origin, None, lo, hi)
+    else:
+        eng.set_messages(origin)
     setup_s = time.perf_counter() - t0
 
 
@@ -131,8 +141,11 @@ def main():
         pg.barrier()
     dt = dist.allmax(pg, time.perf_counter() - t0)
 
-    sends = sum(s["sends"] for r in runs for s in r)   # global (all-reduced) counters
+    sends = sum(s["sends"] for r in runs for s in r)   # vertex partition: global (all-reduced) counters
     rounds = sum(len(r) for r in runs)
+    if shards:   # message shards: every rank counted its own messages' deliveries
+        sends = int(dist.allsum(pg, [float(sends)])[0])
+        rounds = int(dist.allmax(pg, rounds))
     exp_ms = sum(s["expand_ms"] for r in runs for s in r)
     exch_ms = sum(s["exchange_ms"] for r in runs for s in r)
     # roofline of the dominant kernel, k_expand: its pull rounds only, its own
@@ -140,10 +153,12 @@ def main():
     pulls = [s for r in runs for s in r if s["mode"] == 0 and s["kernel_ms"] > 0]
     nbytes = sum(round_bytes(s, eng.words, n) for s in pulls)
     kern_ms = sum(s["kernel_ms"] for s in pulls)
-    if world > 1:   # counters are global (all-reduced): per-rank share for the per-GPU roofline
+    if world > 1 and not shards:   # counters are global (all-reduced): per-rank share for the per-GPU roofline
         nbytes /= world
     achieved = nbytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-    dense_eq = dense_round_bytes(n, nnz, eng.words) * rounds / world / (exp_ms * 1e-3) / 1e9
+    if shards:   # per-GPU roofline: mean over the ranks' own kernels
+        achieved = float(dist.allsum(pg, [achieved])[0]) / world
+    dense_eq = dense_round_bytes(n, nnz, eng.words) * rounds / (1 if shards else world) / (exp_ms * 1e-3) / 1e9
     if args.profile_steps and rank == 0:
         for s in runs[-1]:
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
@@ -172,7 +187,8 @@ def main():
                        "n": n, "arcs": nnz, "mean_degree": nnz / n, "messages": args.messages,
                        "words_per_row": eng.words, "rounds_per_step": rounds / args.steps,
                        "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,
-                       "parallelism": f"vertex-partition x{world}" + (" (RCCL all-gather)" if world > 1 else ""),
+                       "parallelism": (f"message-shard x{world} (no data-path collective)" if shards else
+                                       f"vertex-partition x{world}" + (" (RCCL all-gather)" if world > 1 else "")),
                        "setup_s": round(setup_s, 2)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -183,6 +183,7 @@ struct ExpandArgs {
   int64_t vbegin, nloc;
   int64_t n_items;                     // hub items / hubs for the hub kernels
   int32_t m_total;
+  int32_t wbase;                       // global word index of local word 0 (message shards)
   int32_t rr;                          // receipt round of this expansion (r + 1)
   int32_t hub_thr;
   int32_t vpw;                         // vertices per wave (k_expand)
@@ -202,6 +203,23 @@ constexpr int LIST_SLOTS = 32;   // u16 slots of one 64-byte list segment
 #define EXPAND_BOUNDS __launch_bounds__(BLOCK, GP_EXPAND_WAVES)
 #else
 #define EXPAND_BOUNDS __launch_bounds__(BLOCK)
+#endif
+// EXPERIMENT: cache-policy bits of the gathered row loads (0 = compiler default)
+#ifndef GP_ROW_POLICY
+#define GP_ROW_POLICY 0
+#endif
+#if GP_ROW_POLICY == 1
+#define GP_ROW_POLICY_STR ""
+#elif GP_ROW_POLICY == 2
+#define GP_ROW_POLICY_STR "nt"
+#elif GP_ROW_POLICY == 3
+#define GP_ROW_POLICY_STR "sc1"
+#elif GP_ROW_POLICY == 4
+#define GP_ROW_POLICY_STR "sc0 sc1"
+#elif GP_ROW_POLICY == 5
+#define GP_ROW_POLICY_STR "sc1 nt"
+#elif GP_ROW_POLICY == 6
+#define GP_ROW_POLICY_STR "sc0 sc1 nt"
 #endif
 // rows each lane keeps in flight per gather step (MLP vs VGPRs)
 #ifndef GP_ROWS_IN_FLIGHT
@@ -375,8 +393,20 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, WaveLds& L, int
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
       const int k = k0 + g + q * RPI;
       r[q] = u64x2{0, 0};
+#if GP_ROW_POLICY != 0
+      if constexpr (W >= 2) {   // EXPERIMENT: cache-policy bits on the row loads
+        if (k < cnt) {
+          const u64* p = a.front + (size_t)L.idx[k] * W + lw * 2;
+          asm volatile("global_load_dwordx4 %0, %1, off " GP_ROW_POLICY_STR : "+v"(r[q]) : "v"(p) : "memory");
+        }
+        continue;
+      }
+#endif
       if (k < cnt) r[q] = load_piece<W>(a.front, L.idx[k], lw);
     }
+#if GP_ROW_POLICY != 0
+    if constexpr (W >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 #pragma unroll
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
     st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
@@ -530,8 +560,8 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   if (a.digest) {
     u64 t = 0;
     if (g == 0) {
-      if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(lw * WPL), nw.x);
-      if (WPL == 2 && nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(lw * WPL + 1), nw.y);
+      if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + lw * WPL), nw.x);
+      if (WPL == 2 && nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + lw * WPL + 1), nw.y);
     }
     t = wave_xor_u64(t);
     if (lane == 0) a.digest[i] ^= t;
@@ -1006,6 +1036,7 @@ struct InjectArgs {
   int64_t off, groups;
   int64_t vbegin, vend;
   int32_t words;
+  int32_t wbase;                       // global word index of local word 0 (message shards)
   int32_t r;
 };
 
@@ -1055,7 +1086,7 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
         }
         const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
         if (a.digest) {
-          u64 t = b ? digest_term((uint32_t)a.r, (uint32_t)lane | DIGEST_INJECT, b) : 0ull;
+          u64 t = b ? digest_term((uint32_t)a.r, (uint32_t)(a.wbase + lane) | DIGEST_INJECT, b) : 0ull;
           t = wave_xor_u64(t);
           if (lane == 0) a.digest[i] ^= t;
         }
@@ -1295,6 +1326,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.vbegin = c->vbegin;
   a.nloc = c->nloc();
   a.m_total = c->m;
+  a.wbase = c->cfg.msg_word_base;
   a.rr = c->round + 1;
   a.hub_thr = c->cfg.hub_threshold;
   a.vpw = 4;
@@ -1636,6 +1668,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->reserved0 = 0;
   cfg->sparse_rows = 0;
   cfg->unfiltered_pct = 90;
+  cfg->msg_word_base = 0;
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -1694,6 +1727,7 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->miss_threshold < 1 || cfg->miss_threshold > 254) return set_error(GP_EINVAL, "miss_threshold in [1,254]");
   if (cfg->hub_threshold < 64) return set_error(GP_EINVAL, "hub_threshold must be >= 64");
   if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
+  if (cfg->msg_word_base < 0) return set_error(GP_EINVAL, "msg_word_base < 0");
   GP_HIP(hipSetDevice(c->device));
   const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
   c->cfg = *cfg;
@@ -1981,6 +2015,7 @@ static int round_launch(Ctx* c) {
     ia.vbegin = c->vbegin;
     ia.vend = c->vend;
     ia.words = c->words;
+    ia.wbase = c->cfg.msg_word_base;
     ia.r = r;
     hipLaunchKernelGGL(k_inject, dim3(grid_for(ia.groups, WAVES)), dim3(BLOCK), 0, s, ia);
     GP_HIP(hipGetLastError());

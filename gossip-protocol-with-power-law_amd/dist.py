@@ -1,14 +1,20 @@
-"""Multi-process (one process per GPU) host orchestration.
+"""Multi-process (one process per GPU) host orchestration (DESIGN.md §6).
 
-The data path is RCCL inside libgossip_hip.so (all-gather of the owned next rows
-over xGMI every round); torch.distributed (gloo, CPU) is only the control plane:
-it hands rank 0's RCCL unique id to every rank, aligns the timed region and
-gathers per-rank outputs (the owned slices) for checking.
+Two ways to spread one gossip run over N GPUs:
 
-Partition: rank p owns the contiguous vertex slice [p*S, min((p+1)*S, n)) with
-S = ceil(n / nranks) -- equal-size slices as RCCL's all-gather requires; the
-overlay ids are randomly relabelled, so equal slices carry
-statistically equal arc counts.
+* message shards (default): messages are independent objects -- a message's
+  spread never reads another message's bits -- so rank p runs the whole overlay
+  for the word-aligned message block message_shard(m, N, p).  No data-path
+  collective: the shards' per-round counters add up, their digests XOR, their
+  first / coverage / forwards columns concatenate.
+* vertex partition: rank p owns the contiguous vertex slice [p*S, min((p+1)*S, n))
+  with S = ceil(n / nranks) and every round all-gathers the owned next rows over
+  RCCL inside libgossip_hip.so (equal-size slices as RCCL's all-gather requires;
+  ids are randomly relabelled, DESIGN.md §2.7, so slices carry equal arc counts).
+
+torch.distributed (gloo, CPU) is only the control plane: it hands rank 0's
+RCCL unique id to every rank, aligns the timed region and gathers per-rank
+results for checking.
 """
 import os
 
@@ -19,6 +25,17 @@ def env():
     """(world_size, rank, local_rank) from the torch.distributed.run environment."""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def message_shard(m, nranks, rank):
+    """Word-aligned contiguous message block [lo, hi) of rank `rank`: the
+    m messages are cut into 64-message words, spread as evenly as possible."""
+    words = (m + 63) // 64
+    if nranks > words:
+        raise ValueError(f"{m} messages give {words} words: at most {words} message shards")
+    w0 = rank * words // nranks
+    w1 = (rank + 1) * words // nranks
+    return min(m, 64 * w0), min(m, 64 * w1)
 
 
 def partition_bounds(n, nranks):

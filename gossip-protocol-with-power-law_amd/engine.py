@@ -116,6 +116,17 @@ class GossipEngine:
         self.inject_round = r if r is not None else np.zeros_like(o)
         _, _, self.m, self.words = self.info()
 
+    def set_message_shard(self, origin, inject_round, lo, hi):
+        """Take messages [lo, hi) of a larger message table as this context's
+        shard: local message k is global message lo + k.  lo must
+        be word aligned so that digests of the shards XOR into the digest of
+        the whole table, and first/coverage/forwards concatenate."""
+        if lo % 64:
+            raise ValueError("message shards start on a 64-message word boundary")
+        self.configure(msg_word_base=lo // 64)
+        r = None if inject_round is None else np.asarray(inject_round)[lo:hi]
+        self.set_messages(np.asarray(origin)[lo:hi], r)
+
     def reset(self):
         check(self._lib.gp_reset(self._ctx))
 

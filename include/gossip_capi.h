@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 3
+#define GP_ABI_VERSION 4
 
 typedef struct gp_ctx gp_ctx;
 
@@ -107,6 +107,10 @@ typedef struct gp_config {
                                   64-byte id lists in their row slot   */
   int32_t unfiltered_pct;      /* pull without the per-arc activity check when >= this %
                                   of vertices are senders (0 = never)   */
+  int32_t msg_word_base;       /* message shards: this context's message k
+                                  is global message 64*msg_word_base + k; the digest uses
+                                  global word indices, so shard digests XOR together     */
+  int32_t pad;
 } gp_config;
 
 /* what for gp_read */

@@ -78,6 +78,27 @@ def digest_term(rr, w, bits):
     return int(load().or_digest_term(rr, w, bits))
 
 
+def digest_from_first(first, origin, word_base=0):
+    """Per-vertex digest recomputed from a first-receipt matrix
+    [n][m] whose column k is global message 64*word_base + k -- the digest of a
+    message shard in global word numbering (shard digests XOR together)."""
+    n, m = first.shape
+    own = {}
+    for k in range(m):
+        own.setdefault(int(origin[k]), set()).add(k)
+    out = np.zeros(n, np.uint64)
+    for v in range(n):
+        groups = {}
+        for k in np.nonzero(first[v] != 255)[0]:
+            key = (int(first[v, k]), int(k) >> 6, int(k) in own.get(v, ()))
+            groups[key] = groups.get(key, 0) | (1 << (int(k) & 63))
+        d = 0
+        for (rr, w, inj), bits in groups.items():
+            d ^= digest_term(rr, (word_base + w) | (0x80000000 if inj else 0), bits)
+        out[v] = d
+    return out
+
+
 def run(csr, origin, inject_round=None, churn=False, p_fail=0.0, churn_seed=0, miss_threshold=3,
         crashes=(), max_rounds=254, nthreads=1, want_first=False, want_forwards=True,
         report_cap=1 << 20):

@@ -70,3 +70,80 @@ def test_partition_bounds(pkg):
         assert all(b[i][1] == b[i + 1][0] for i in range(p - 1))
         s = (n + p - 1) // p
         assert all(e - s0 <= s for s0, e in b)
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import _gossip_pkg
+    from oracle import lib as oracle
+    pkg = _gossip_pkg.load()
+    d = pkg.dist
+    pg = d.init("gloo")
+    try:
+        g = pkg.overlay.barabasi_albert(700, 2, seed=6)
+        m = 200
+        origin = pkg.overlay.random_origins(g.n, m, 6)
+        inject = (np.arange(m) % 3).astype(np.int32)
+        full = oracle.run(g, origin, inject, want_first=True)
+        lo, hi = d.message_shard(m, world, rank)
+        part = oracle.run(g, origin[lo:hi], inject[lo:hi], want_first=True)
+        # per-round counters add up (pad the shorter shard runs with quiet rounds)
+        R = 64
+        loc = np.zeros((R, 2))
+        for i, s in enumerate(part["stats"]):
+            loc[i] = (s["new_bits"], s["sends"])
+        tot = d.allsum(pg, loc)
+        ok_rounds = all(tot[i, 0] == s["new_bits"] and tot[i, 1] == s["sends"]
+                        for i, s in enumerate(full["stats"]))
+        # columns concatenate, digests (global word numbering) XOR
+        first = np.concatenate([x for x in _gather(pg, part["first"].T)]).T
+        dig = 0
+        for x in _gather(pg, oracle.digest_from_first(part["first"], origin[lo:hi], lo // 64)):
+            dig = np.bitwise_xor(dig, x)
+        cov = np.concatenate(_gather(pg, part["coverage"]))
+        q.put((rank, ok_rounds, np.array_equal(first, full["first"]), np.array_equal(dig, full["digest"]),
+               np.array_equal(cov, full["coverage"])))
+    finally:
+        pg.destroy_process_group()
+
+
+def _gather(pg, x):
+    parts = [None] * pg.get_world_size()
+    pg.all_gather_object(parts, np.asarray(x))
+    return parts
+
+
+def test_two_rank_message_shards_compose():
+    """Message shards (the default multi-GPU decomposition): two
+    ranks each run the oracle on their word-aligned message block; per-round
+    counters sum, first-receipt columns and coverage concatenate and the
+    shard digests (global word numbering) XOR to the whole run's."""
+    mp = pytest.importorskip("torch.multiprocessing")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, *oks in res:
+        assert all(oks), (rank, oks)
+
+
+def test_message_shard_bounds(pkg):
+    d = pkg.dist
+    for m, p in [(4096, 1), (4096, 2), (4096, 8), (200, 2), (130, 3), (64, 1)]:
+        b = [d.message_shard(m, p, r) for r in range(p)]
+        assert b[0][0] == 0 and b[-1][1] == m
+        assert all(b[i][1] == b[i + 1][0] for i in range(p - 1))
+        assert all(lo % 64 == 0 for lo, _ in b)
+    assert d.message_shard(4096, 8, 3) == (1536, 2048)
+    with pytest.raises(ValueError):
+        d.message_shard(100, 3, 0)

@@ -284,3 +284,44 @@ def test_wide_rows_sparse_format(pkg, oracle, mode, sparse_rows):
     else:
         assert sum(s["sparse_written"] for s in r["stats"]) == 0
     r["eng"].close()
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_message_shards_match_whole_run(pkg, shards):
+    """Message shards on one GPU, one context each: the per-round
+    sends and new bits add up to the whole run's, coverage / forwards / first
+    columns concatenate, and the shard digests XOR to the whole run's digest."""
+    rp, col = pkg_oracle_chung_lu(20_000, 8, 2.4, 13)
+    g = pkg.CSR(20_000, rp, col, False)
+    m = 1024
+    origin = pkg.overlay.random_origins(g.n, m, seed=13)
+    inject = (np.arange(m) % 3).astype(np.int32)
+
+    def run(lo, hi):
+        eng = pkg.GossipEngine(0, track_first=1, track_digest=1)
+        eng.load_graph(g)
+        eng.set_message_shard(origin, inject, lo, hi)
+        eng.reset()
+        stats = eng.run()
+        eng.finalize()
+        out = (stats, eng.first(), eng.digest(), eng.coverage(), eng.forwards())
+        eng.close()
+        return out
+
+    whole = run(0, m)
+    parts = [run(*pkg.dist.message_shard(m, shards, r)) for r in range(shards)]
+    for i, s in enumerate(whole[0]):
+        for k in ("new_bits", "sends", "injected"):
+            assert s[k] == sum(p[0][i][k] if i < len(p[0]) else 0 for p in parts), (k, i)
+    assert np.array_equal(np.concatenate([p[1] for p in parts], axis=1), whole[1])
+    dig = np.zeros_like(whole[2])
+    for p in parts:
+        dig ^= p[2]
+    assert np.array_equal(dig, whole[2])
+    assert np.array_equal(np.concatenate([p[3] for p in parts]), whole[3])
+    assert np.array_equal(np.concatenate([p[4] for p in parts]), whole[4])
+
+
+def pkg_oracle_chung_lu(n, dbar, gamma, seed):
+    from oracle import lib as oracle
+    return oracle.chung_lu(n, dbar, gamma, seed)
