@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--early-exit", type=int, default=1)
     ap.add_argument("--unfiltered-pct", type=int, default=90,
                     help="pull without the per-arc activity check when >= this %% of vertices send (0 = never)")
+    ap.add_argument("--flat-max-words", type=int, default=16,
+                    help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--sparse-rows", type=int, default=0,
                     help="store frontier rows with <= 32 new bits as id lists (W >= 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -108,7 +110,7 @@ def main():
     eng = pkg.GossipEngine(device, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
                            push_ratio=args.push_ratio,
                            early_exit=args.early_exit, sparse_rows=args.sparse_rows,
-                           unfiltered_pct=args.unfiltered_pct)
+                           unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()

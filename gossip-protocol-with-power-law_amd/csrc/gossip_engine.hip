@@ -639,6 +639,221 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
   flush_stats(st, a.partial);
 }
 
+// ---------------------------------------------------------------------------
+// edge-parallel pull for narrow rows (W <= 32: message shards, C2/C3 widths).
+// The per-receiver loop of k_expand pays several dependent memory round trips
+// per receiver, which narrow rows cannot amortise.  Here a wave streams the
+// in-arcs of all its (non-hub) receivers as one flat sequence: QA chunks of 64
+// arcs have their column ids and activity probes in flight together, the
+// active rows are gathered RPI per wave-instruction whatever receiver they
+// belong to, and OR-ed into per-receiver accumulators in LDS (ds_or_b64).  The
+// receiver side then runs lane-parallel, one receiver per lane.  No early exit
+// (narrow rows are cheap next to the arc scan); id-list rows are not read here
+// (the per-receiver kernel takes rounds that may hold them).
+constexpr int FLAT_CAP = 512;   // arc positions per owner window
+// row wave-instructions in flight per lane (VGPRs vs occupancy: 2 -> 66 VGPRs at W = 8)
+#ifndef GP_FLAT_ROWS_IN_FLIGHT
+#define GP_FLAT_ROWS_IN_FLIGHT 2
+#endif
+template <int W>
+struct FlatLds {
+  u64 acc[64][W];               // OR accumulators of the wave's 64 receivers
+  int32_t idx[64];              // active neighbours of one chunk
+  int8_t vtx[64];               // their receiver (lane) in the wave
+  int8_t own[FLAT_CAP];         // receiver lane owning each arc position of the window
+};
+
+template <int W, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
+  constexpr int LPR = Geo<W>::LPR;
+  constexpr int RPI = Geo<W>::RPI;
+  constexpr int WPL = Geo<W>::WPL;
+  constexpr int QA = 4;
+  __shared__ FlatLds<W> s_f[WAVES];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  FlatLds<W>& F = s_f[wib];
+  WaveStats st;
+  ws_zero(st);
+  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
+  if (base < a.nloc) {
+    const int64_t li = base + lane;
+    bool need = false, act = false;
+    u64 sends = 0;
+    uint32_t sp = 0, deg = 0;
+    int64_t vb = 0;
+    int v = 0;
+    if (li < a.nloc) {
+      v = (int)(a.vbegin + li);
+      const uint32_t fp = a.fpop[v];
+      act = fp != 0u;
+      if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
+      vb = a.row_ptr[v];
+      const int64_t e = a.row_ptr[v + 1];
+      const bool hub = e - vb > a.hub_thr;   // split over waves by the hub kernels
+      sp = a.seenpop[li];
+      need = !(a.state[v] & ST_DOWN) && sp < a.done_at[v] && !hub && e > vb;
+      if (!need && !hub) a.fpop_next[v] = 0;
+      deg = (uint32_t)(e - vb);
+    }
+    st.add(S_SENDS, wave_sum_u64(sends));
+    st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
+    st.add(S_VISITED, (u64)__popcll(__ballot(need)));
+#pragma unroll
+    for (int w = 0; w < W; ++w) F.acc[lane][w] = 0ull;
+    const uint32_t sdeg = need ? deg : 0u;
+    const uint32_t excl = wave_excl_scan_u32(sdeg, lane);
+    const uint32_t incl = excl + sdeg;
+    const uint32_t T = (uint32_t)__shfl((int)incl, 63);
+    const uint32_t vb_lo = (uint32_t)vb, vb_hi = (uint32_t)((u64)vb >> 32);
+    st.add(S_ARCS, T);
+    u64 gathered = 0;
+    for (uint32_t g0 = 0; g0 < T; g0 += FLAT_CAP) {
+      const uint32_t wn = min((uint32_t)FLAT_CAP, T - g0);
+      // owner table of positions [g0, g0 + wn): start markers, then a forward
+      // fill seeded with the receiver that straddles g0
+      {
+        u64* own8 = reinterpret_cast<u64*>(F.own);
+        own8[lane] = 0xFFFFFFFFFFFFFFFFull;
+        wave_sync_lds();
+        if (sdeg && excl >= g0 && excl < g0 + wn) F.own[excl - g0] = (int8_t)lane;
+        const u64 before = __ballot(sdeg && excl < g0);
+        const int carry_in = before ? 63 - __clzll((long long)before) : -1;
+        wave_sync_lds();
+        const u64 w8 = own8[lane];
+        int run = -1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int o = (int8_t)((w8 >> (8 * q)) & 0xFF);
+          if (o >= 0) run = o;
+        }
+        int carry = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(carry, o);
+          if (lane >= o) carry = max(carry, y);
+        }
+        int cur = __shfl_up(carry, 1);
+        if (lane == 0) cur = carry_in;
+        cur = max(cur, carry_in);
+        u64 out = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int o = (int8_t)((w8 >> (8 * q)) & 0xFF);
+          if (o >= 0) cur = o;
+          out |= (u64)(uint8_t)(int8_t)cur << (8 * q);
+        }
+        own8[lane] = out;
+        wave_sync_lds();
+      }
+      for (uint32_t c0 = 0; c0 < wn; c0 += 64 * QA) {
+        int32_t col[QA];
+        int8_t who[QA];
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+          const uint32_t p = c0 + (uint32_t)(q * 64 + lane);
+          const int j = p < wn ? (int)F.own[p] : 0;
+          // shuffles with the whole wave active (bpermute reads every lane)
+          const int64_t b = (int64_t)(((u64)(uint32_t)__shfl((int)vb_hi, j) << 32) |
+                                      (u64)(uint32_t)__shfl((int)vb_lo, j));
+          const uint32_t s = (uint32_t)__shfl((int)excl, j);
+          who[q] = (int8_t)j;
+          col[q] = -1;
+          if (p < wn) col[q] = a.gcol[b + (g0 + p - s)];
+        }
+        u64 raw[QA];   // activity words (no list rows in this kernel)
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+          raw[q] = 0;
+          if constexpr (MODE != SCAN_UNFILTERED)
+            if (col[q] >= 0) raw[q] = reinterpret_cast<const u64*>(a.bits2)[(col[q] >> 6) * 2];
+        }
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+          const int32_t u = col[q] >= 0 ? classify<MODE>(u64x2{raw[q], 0}, col[q]) : -1;
+          const u64 am = __ballot(u >= 0);
+          const int cnt = __popcll(am);
+          if (cnt == 0) continue;
+          if (u >= 0) {
+            const int r = lane_rank(am);
+            F.idx[r] = u;
+            F.vtx[r] = who[q];
+          }
+          wave_sync_lds();
+          gathered += (u64)cnt;
+          for (int k0 = 0; k0 < cnt; k0 += GP_FLAT_ROWS_IN_FLIGHT * RPI) {
+            u64x2 r[GP_FLAT_ROWS_IN_FLIGHT];
+#pragma unroll
+            for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
+              const int k = k0 + g + t * RPI;
+              r[t] = u64x2{0, 0};
+              if (k < cnt) r[t] = load_piece<W>(a.front, F.idx[k], lw);
+            }
+#pragma unroll
+            for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
+              const int k = k0 + g + t * RPI;
+              if (k < cnt) {
+                u64* dst = &F.acc[F.vtx[k]][lw * WPL];
+                if (r[t].x) atomicOr(dst, r[t].x);
+                if constexpr (WPL == 2) {
+                  if (r[t].y) atomicOr(dst + 1, r[t].y);
+                }
+              }
+            }
+          }
+          wave_sync_lds();
+        }
+      }
+    }
+    st.add(S_GATHERED, gathered);
+    // receiver side, one receiver per lane
+    u64 nbits = 0, nrecv = 0, nwritten = 0, narcs = 0, nseen = 0;
+    if (need) {
+      u64 any = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) any |= F.acc[lane][w];
+      if (!any) {
+        a.fpop_next[v] = 0;
+      } else {
+        if (sp) nseen = 1;
+        uint32_t tot = 0;
+        u64 dig = 0;
+        u64* __restrict__ nrow = a.next + (size_t)v * W;
+        u64* __restrict__ srow = a.seen + (size_t)li * W;
+        uint8_t* __restrict__ frow = a.first ? a.first + (size_t)li * (W * 64) : nullptr;
+#pragma unroll 2
+        for (int w = 0; w < W; ++w) {
+          const u64 s = sp ? srow[w] : 0ull;
+          const u64 nw = F.acc[lane][w] & ~s;
+          nrow[w] = nw;
+          if (nw || !sp) srow[w] = s | nw;   // a row first written this run is written whole
+          if (nw) {
+            tot += (uint32_t)__popcll(nw);
+            if (a.digest) dig ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + w), nw);
+            if (frow) set_first_bytes(frow, w, nw, (uint32_t)a.rr);
+          }
+        }
+        a.fpop_next[v] = tot;
+        if (tot) {
+          a.seenpop[li] = sp + tot;
+          if (a.digest) a.digest[li] ^= dig;
+          nbits = tot;
+          nrecv = 1;
+          nwritten = 1;
+          narcs = (u64)(uint32_t)max(a.deg_live[v], 0);
+        }
+      }
+    }
+    st.add(S_NEW_BITS, wave_sum_u64(nbits));
+    st.add(S_RECEIVERS, wave_sum_u64(nrecv));
+    st.add(S_WRITTEN, wave_sum_u64(nwritten));
+    st.add(S_NEXT_ARCS, wave_sum_u64(narcs));
+    st.add(S_SEEN_READ, wave_sum_u64(nseen));
+  }
+  flush_stats(st, a.partial);
+}
+
 // hubs, pass 1: one wave per (hub, arc chunk) -> partial OR row
 template <int W, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
@@ -1367,7 +1582,17 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   // injection wrote some
   const int mode = a.unfiltered ? SCAN_UNFILTERED : (c->lists_live ? SCAN_LISTS : SCAN_FILTERED);
   (void)hipEventRecord(c->ev[4], c->stream);
-  if (a.nloc > 0) {
+  // (the flat kernel writes bitmap rows only: not while id-list rows are configured)
+  const bool flat = W <= 32 && W <= c->cfg.flat_max_words && c->list_max() == 0;
+  if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
+    const dim3 grid(grid_for(a.nloc, per_block));
+    if constexpr (W <= 32) {
+      if (mode == SCAN_UNFILTERED)
+        hipLaunchKernelGGL((k_expand_flat<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+      else
+        hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+    }
+  } else if (a.nloc > 0) {
     const dim3 grid(grid_for(a.nloc, per_block));
     if (mode == SCAN_UNFILTERED)
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
@@ -1669,6 +1894,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->sparse_rows = 0;
   cfg->unfiltered_pct = 90;
   cfg->msg_word_base = 0;
+  cfg->flat_max_words = 16;
 }
 
 int gp_create(int device, gp_ctx** out) {

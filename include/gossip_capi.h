@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 4
+#define GP_ABI_VERSION 5
 
 typedef struct gp_ctx gp_ctx;
 
@@ -110,7 +110,8 @@ typedef struct gp_config {
   int32_t msg_word_base;       /* message shards: this context's message k
                                   is global message 64*msg_word_base + k; the digest uses
                                   global word indices, so shard digests XOR together     */
-  int32_t pad;
+  int32_t flat_max_words;      /* rows of at most this many words (<= 32) take the
+                                  edge-parallel pull kernel (0 = never)  */
 } gp_config;
 
 /* what for gp_read */
