@@ -149,7 +149,8 @@ struct ExpandArgs {
   const int32_t* __restrict__ col;
   const u64* __restrict__ front;       // frontier_r
   const uint32_t* __restrict__ fpop;   // |frontier_r|
-  const u64x2* __restrict__ bits2;     // per 64 vertices {active: fpop != 0, list row: 1 <= fpop <= list_max}
+  const u64* __restrict__ abits;       // bit v: frontier_r(v) != 0 (2 MB at 2^24; one word per 64 vertices)
+  const u64* __restrict__ sbits;       // bit v: frontier_r(v) is an id-list row (1 <= fpop <= list_max)
   int32_t list_max;                    // frontier rows with <= list_max bits are id lists (0: none)
   const int32_t* __restrict__ gcol;    // in-CSR columns in gather order (neighbour degree desc)
   const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
@@ -322,9 +323,9 @@ __device__ __forceinline__ u64x2 probe_raw(const ExpandArgs& a, int32_t u) {
   if constexpr (MODE == SCAN_UNFILTERED) {   // dense round: no bitmap probe (it misses L2 under the row stream)
     return u64x2{0, 0};
   } else if constexpr (MODE == SCAN_LISTS) {  // one 16-byte probe: activity + list format
-    return a.bits2[u >> 6];
+    return u64x2{a.abits[u >> 6], a.sbits[u >> 6]};
   } else {
-    return u64x2{reinterpret_cast<const u64*>(a.bits2)[(u >> 6) * 2], 0};
+    return u64x2{a.abits[u >> 6], 0};
   }
 }
 template <int MODE>
@@ -767,7 +768,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
         for (int q = 0; q < QA; ++q) {
           raw[q] = 0;
           if constexpr (MODE != SCAN_UNFILTERED)
-            if (col[q] >= 0) raw[q] = reinterpret_cast<const u64*>(a.bits2)[(col[q] >> 6) * 2];
+            if (col[q] >= 0) raw[q] = a.abits[col[q] >> 6];
         }
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
@@ -925,14 +926,14 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
 
 // active senders from the bitmap: one thread per 64-vertex word, block-level
 // compaction, one cursor add per block; big senders go to their own list
-__global__ __launch_bounds__(BLOCK) void k_active_list(const u64x2* __restrict__ bits2, int64_t nwords,
+__global__ __launch_bounds__(BLOCK) void k_active_list(const u64* __restrict__ abits, int64_t nwords,
                                                        const int64_t* __restrict__ orp, int32_t big_thr,
                                                        int32_t* __restrict__ active, int32_t* __restrict__ big,
                                                        u64* __restrict__ stats) {
   __shared__ uint32_t s_cnt[BLOCK];
   __shared__ u64 s_base;
   const int64_t w = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const u64 bits = w < nwords ? bits2[w].x : 0ull;
+  const u64 bits = w < nwords ? abits[w] : 0ull;
   s_cnt[threadIdx.x] = (uint32_t)__popcll(bits);
   __syncthreads();
   for (int o = 1; o < BLOCK; o <<= 1) {   // inclusive scan
@@ -1137,7 +1138,8 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
 // frontier bitmaps, interleaved per 64 vertices so one 16-byte probe answers
 // both questions: .x bit = (fpop != 0), .y bit = id-list row (1 <= fpop <= list_max)
 __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, int32_t list_max,
-                                                  u64x2* __restrict__ bits2, int64_t n) {
+                                                  u64* __restrict__ abits, u64* __restrict__ sbits,
+                                                  int64_t n) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
@@ -1145,7 +1147,10 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
     const uint32_t fp = v < n ? fpop[v] : 0u;
     const u64 m = __ballot(fp != 0u);
     const u64 sm = __ballot(is_list_row(fp, list_max));
-    if (lane == 0) bits2[v0 >> 6] = u64x2{m, sm};
+    if (lane == 0) {
+      abits[v0 >> 6] = m;
+      sbits[v0 >> 6] = sm;
+    }
   }
 }
 
@@ -1154,13 +1159,13 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
 // or crashed) become zero, id-list rows are expanded to bitmap rows.  One wave
 // per 64-vertex bitmap word; fully active dense words cost one load.
 template <int W>
-__global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64x2* __restrict__ bits2,
+__global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64* __restrict__ abits, const u64* __restrict__ sbits,
                                                       const uint32_t* __restrict__ fpop, int32_t list_max,
                                                       u64* __restrict__ front, int64_t n_alloc) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
   if (w * 64 >= n_alloc) return;
-  const u64x2 pb = bits2[w];
+  const u64x2 pb = u64x2{abits[w], sbits[w]};
   u64 todo = ~pb.x | pb.y;
   while (todo) {
     const int b = __ffsll((long long)todo) - 1;
@@ -1517,7 +1522,8 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.col = c->d_col;
   a.front = c->d_front[c->cur];
   a.fpop = c->d_fpop[c->cur];
-  a.bits2 = c->d_bits2;
+  a.abits = c->d_abits;
+  a.sbits = c->d_sbits;
   a.list_max = c->list_max();
   a.done_at = c->d_done_at;
   a.gcol = c->d_gcol;
@@ -1559,7 +1565,7 @@ template <int W>
 static void launch_push_w(Ctx* c, ExpandArgs a) {
   hipStream_t s = c->stream;
   const int64_t nwords = (c->n_alloc + 63) / 64;
-  hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_bits2, nwords,
+  hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_abits, nwords,
                      a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats);
   hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, a);
@@ -1577,7 +1583,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   const int64_t per_block = (int64_t)WAVES * 64;
   if (a.unfiltered)
     hipLaunchKernelGGL(k_fixup_rows<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
-                       c->d_bits2, c->d_fpop[c->cur], a.list_max, c->d_front[c->cur], c->n_alloc);
+                       c->d_abits, c->d_sbits, c->d_fpop[c->cur], a.list_max, c->d_front[c->cur], c->n_alloc);
   // id-list rows can only be present if the last round or this round's
   // injection wrote some
   const int mode = a.unfiltered ? SCAN_UNFILTERED : (c->lists_live ? SCAN_LISTS : SCAN_FILTERED);
@@ -1619,7 +1625,8 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 
 static int launch_expand(Ctx* c) {
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
-                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->list_max(), c->d_bits2, c->n_alloc);
+                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->list_max(), c->d_abits, c->d_sbits,
+                     c->n_alloc);
   // direction: push when the senders' arcs are a small share of all arcs
   const int r = c->round;
   // early exit pays once frontier rows are dense: >= m/16 new bits per vertex last round
@@ -1728,7 +1735,7 @@ static void free_state(Ctx* c) {
   }
   dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_bits2); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_done_at);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
@@ -1779,7 +1786,8 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_miss, na));
   GP_TRY(dalloc(&c->d_deg_live, na));
   GP_TRY(dalloc(&c->d_cand, na));
-  GP_TRY(dalloc(&c->d_bits2, (na + 63) / 64));
+  GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
+  GP_TRY(dalloc(&c->d_sbits, (na + 63) / 64));
   GP_TRY(dalloc(&c->d_done_at, na));
   c->done_at_valid = false;
   GP_TRY(dalloc(&c->d_acc, na * W));
@@ -1931,7 +1939,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_bits2); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_done_at);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);

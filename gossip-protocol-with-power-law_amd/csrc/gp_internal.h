@@ -83,8 +83,10 @@ struct Ctx {
   uint8_t* d_miss = nullptr;        // [n_alloc]
   int32_t* d_deg_live = nullptr;    // [n_alloc]
   int32_t* d_cand = nullptr;        // [n] detection candidates of a round
-  // [n_alloc/64] per 64 vertices {active bits, id-list-row bits} of frontier_r
-  u64 __attribute__((ext_vector_type(2)))* d_bits2 = nullptr;
+  // [n_alloc/64] frontier_r bitmaps: active rows (fpop != 0) and id-list rows;
+  // separate arrays so the per-arc activity probe touches only 2 MB at 2^24
+  u64* d_abits = nullptr;
+  u64* d_sbits = nullptr;
   // push (sparse-round) mode
   u64* d_acc = nullptr;             // [n_alloc][W] OR accumulator, kept all-zero between uses
   u64* d_tbits = nullptr;           // [n_alloc/64] receivers pushed to this round

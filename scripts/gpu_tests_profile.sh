@@ -1,0 +1,7 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest exit $rc"; tail -2 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+bash scripts/gpu_round_profile.sh

@@ -1,9 +1,14 @@
 #!/usr/bin/env python3
-"""Per-dispatch HBM traffic of the gossip kernels from two rocprofv3 --pmc passes
-(FETCH_SIZE, WRITE_SIZE; KB units) next to the algorithmic bytes of each round.
-gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the
-bytes of wide coalesced reads, so fetched bytes = 2 x FETCH_SIZE x 1024.
-usage: pmc_summary.py <dir with fetch/ write/ subdirs and fetch.err>"""
+"""Per-dispatch HBM traffic of k_expand from two rocprofv3 --pmc passes
+(FETCH_SIZE and WRITE_SIZE in KB; they cannot share a pass on gfx950) next to
+the algorithmic bytes of the same rounds (bench.round_bytes).
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts the
+128-B read requests at 64 B, so fetched bytes = 2 x FETCH_SIZE x 1024
+(checked here: TCC_EA0_RDREQ_128B x 128 B gives the same figure).  Infinity
+Cache hits are counted, not excluded, so this is L2-to-fabric traffic.
+
+usage: pmc_summary.py <dir holding fetch/ write/ and fetch.err> [json_out]"""
 import csv
 import glob
 import json
@@ -15,14 +20,13 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 def load(d, counter):
     path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-    out = []
+    per = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
+        if r["Counter_Name"] != counter or "k_expand" not in r["Kernel_Name"]:
             continue
-        out.append((int(r["Dispatch_Id"]), r["Kernel_Name"].split("(")[0].replace("void ", ""),
-                    float(r["Counter_Value"])))
-    out.sort()
-    return out
+        k = int(r["Dispatch_Id"])
+        per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
+    return [per[k] for k in sorted(per)]
 
 
 def main():
@@ -30,34 +34,34 @@ def main():
     fetch = load(os.path.join(d, "fetch"), "FETCH_SIZE")
     write = load(os.path.join(d, "write"), "WRITE_SIZE")
     rounds = [json.loads(l) for l in open(os.path.join(d, "fetch.err")) if l.startswith("{")]
+    bench = json.loads(open(os.path.join(d, "fetch.json")).read())
     from bench import round_bytes
-    words = 64
-    n = 1 << 24
-    ex_f = [(k, v) for _, k, v in fetch if "k_expand" in k]
-    ex_w = [(k, v) for _, k, v in write if "k_expand" in k]
-    pull = [r for r in rounds if r["mode"] == 0]
-    print("| round | kernel | alg GB | fetch GB (2x FETCH_SIZE) | write GB | HBM GB | HBM / alg |")
-    print("|---|---|---|---|---|---|---|")
-    tot_a = tot_h = 0.0
-    for r, (k, f), (_, w) in zip(pull, ex_f, ex_w):
-        alg = round_bytes(r, words, n) / 1e9
-        fg, wg = 2 * f * 1024 / 1e9, w * 1024 / 1e9
-        tot_a += alg
-        tot_h += fg + wg
-        print(f"| {r['round']} | {k} | {alg:.2f} | {fg:.2f} | {wg:.2f} | {fg + wg:.2f} | {(fg + wg) / alg:.3f} |")
-    print(f"| all pull | k_expand | {tot_a:.2f} | | | {tot_h:.2f} | {tot_h / max(tot_a, 1e-9):.3f} |")
-    print()
-    agg = {}
-    for lst, key in ((fetch, "f"), (write, "w")):
-        for _, k, v in lst:
-            a = agg.setdefault(k, {"f": 0.0, "w": 0.0, "n": 0})
-            a[key] += v
-            if key == "f":
-                a["n"] += 1
-    print("| kernel | dispatches | fetch GB (2x) | write GB |")
-    print("|---|---|---|---|")
-    for k, a in sorted(agg.items(), key=lambda x: -x[1]["f"]):
-        print(f"| `{k}` | {a['n']} | {2 * a['f'] * 1024 / 1e9:.2f} | {a['w'] * 1024 / 1e9:.2f} |")
+    words = bench["config"]["words_per_row"]
+    n = bench["config"]["n"]
+    pull = [r for r in rounds if r["mode"] == 0 and r.get("kernel_ms", 0) > 0]
+    assert len(pull) == len(fetch) == len(write), (len(pull), len(fetch), len(write))
+    rows = []
+    for r, f, w in zip(pull, fetch, write):
+        rows.append({"round": r["round"], "alg_GB": round_bytes(r, words, n) / 1e9,
+                     "fetch_GB": 2 * f * 1024 / 1e9, "write_GB": w * 1024 / 1e9,
+                     "kernel_ms": r["kernel_ms"]})
+    print("| round | alg GB | fetch GB (2 x FETCH_SIZE) | write GB | HBM GB | HBM / alg | kernel ms | HBM TB/s |")
+    print("|---|---|---|---|---|---|---|---|")
+    for x in rows:
+        h = x["fetch_GB"] + x["write_GB"]
+        print(f"| {x['round']} | {x['alg_GB']:.2f} | {x['fetch_GB']:.2f} | {x['write_GB']:.2f} | {h:.2f} | "
+              f"{h / x['alg_GB']:.3f} | {x['kernel_ms']:.2f} | {h / x['kernel_ms']:.2f} |")
+    ta = sum(x["alg_GB"] for x in rows)
+    th = sum(x["fetch_GB"] + x["write_GB"] for x in rows)
+    tm = sum(x["kernel_ms"] for x in rows)
+    print(f"| all {len(rows)} launches | {ta:.2f} | | | {th:.2f} | {th / ta:.3f} | {tm:.2f} | {th / tm:.2f} |")
+    out = {"kernel": "k_expand", "launches": len(rows), "traffic_bytes_per_launch": th * 1e9 / len(rows),
+           "alg_bytes_per_launch": ta * 1e9 / len(rows), "kernel_ms_per_launch": tm / len(rows),
+           "rounds": rows, "config": bench["config"],
+           "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bytes = "
+                     "2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (MI355X_MICROARCH.md gfx950 correction)"}
+    if len(sys.argv) > 2:
+        json.dump(out, open(sys.argv[2], "w"), indent=1)
 
 
 if __name__ == "__main__":
