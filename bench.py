@@ -44,8 +44,6 @@ def parse():
                     help="pull without the per-arc activity check when >= this %% of vertices send (0 = never)")
     ap.add_argument("--flat-max-words", type=int, default=16,
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
-    ap.add_argument("--sparse-rows", type=int, default=0,
-                    help="store frontier rows with <= 32 new bits as id lists (W >= 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-messages", type=int, default=64)
@@ -57,21 +55,35 @@ def parse():
     return ap.parse_args()
 
 
-SPARSE_ROW_BYTES = 64   # id-list row: 32 u16 message ids
-
-
 def round_bytes(st, words, nloc):
-    """Algorithmic bytes of one expansion launch of the sparse-aware pull
-    (DESIGN.md §3.2): per owned vertex 21 B of vertex state, per scanned arc 8 B
-    (column id + the neighbour's activity bit), per gathered frontier row 8W B
-    (64 B when it is an id list), per receiver seen row read 8W B, per written
-    row 8W B of seen plus 8W B of next (64 B when next is an id list)."""
+    """Algorithmic bytes of one expansion launch of the pull:
+    per owned vertex 21 B of vertex state (fpop, deg_live, row_ptr pair, state,
+    seenpop, done_at, slot byte), per scanned arc the 4-B column id (+ 8 B for
+    the activity-bitmap probe in filtered rounds), per gathered neighbour row
+    8W B, per receiver seen row read 8W B and per receiver seen row written
+    to the next slot 8W B."""
     w8 = 8 * words
-    sg, sw = st.get("sparse_gathered", 0), st.get("sparse_written", 0)
-    gathered = w8 * (st["rows_gathered"] - sg) + SPARSE_ROW_BYTES * sg
-    written = w8 * st["rows_written"] + w8 * (st["rows_written"] - sw) + SPARSE_ROW_BYTES * sw
-    arc = 4 if st.get("unfiltered") else 8   # column id (+ activity-bitmap probe when filtered)
-    return 21 * nloc + arc * st["arcs_scanned"] + gathered + w8 * st["seen_rows_read"] + written
+    arc = 4 if st.get("unfiltered") else 12
+    return (21 * nloc + arc * st["arcs_scanned"] + w8 * st["rows_gathered"] + w8 * st["seen_rows_read"]
+            + w8 * st["rows_written"])
+
+
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(config):
+    """HBM traffic per k_expand launch measured by the two rocprofv3 --pmc
+    passes of scripts/gpu_round_profile.sh (FETCH_SIZE x2 + WRITE_SIZE, the
+    gfx950 correction of MI355X_MICROARCH.md), for this exact workload; None
+    when no such measurement is committed under profiles/."""
+    try:
+        d = json.load(open(PMC_TRAFFIC))
+    except (OSError, ValueError):
+        return None, None
+    keys = ("n", "arcs", "messages", "words_per_row", "seed", "parallelism")
+    if any(d["config"].get(k) != config.get(k) for k in keys):
+        return None, None
+    return d["traffic_bytes_per_launch"], os.path.relpath(PMC_TRAFFIC, ROOT)
 
 
 def dense_round_bytes(n, nnz, words):
@@ -109,7 +121,7 @@ def main():
     device = local % max(pkg._lib.device_count(), 1)
     eng = pkg.GossipEngine(device, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
                            push_ratio=args.push_ratio,
-                           early_exit=args.early_exit, sparse_rows=args.sparse_rows,
+                           early_exit=args.early_exit,
                            unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
@@ -165,7 +177,7 @@ def main():
         for s in runs[-1]:
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
-                                                "rows_written", "sparse_gathered", "sparse_written", "atomics",
+                                                "rows_written", "atomics",
                                                 "unfiltered", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None
@@ -203,6 +215,11 @@ def main():
                          "exchange_ms_per_round": exch_ms / rounds},
             "cpu_baseline": cpu,
         }
+        traffic, src = pmc_traffic(out["config"])
+        if traffic is not None:
+            out["roofline"]["traffic"] = traffic
+            out["roofline"]["traffic_source"] = src
+            out["roofline"]["traffic_over_alg"] = traffic / out["roofline"]["alg_bytes_per_launch"]
         print(json.dumps(out), flush=True)
     eng.close()
     if pg is not None:

@@ -47,8 +47,6 @@ class RoundStats(ctypes.Structure):
         ("vertices_visited", ctypes.c_uint64),
         ("atomics", ctypes.c_uint64),
         ("next_arcs", ctypes.c_uint64),
-        ("sparse_gathered", ctypes.c_uint64),
-        ("sparse_written", ctypes.c_uint64),
         ("mode", ctypes.c_int32),
         ("unfiltered", ctypes.c_int32),
         ("expand_ms", ctypes.c_double),
@@ -79,7 +77,7 @@ class Config(ctypes.Structure):
         ("push_ratio", ctypes.c_double),
         ("early_exit", ctypes.c_int32),
         ("reserved0", ctypes.c_int32),
-        ("sparse_rows", ctypes.c_int32),
+        ("reserved1", ctypes.c_int32),
         ("unfiltered_pct", ctypes.c_int32),
         ("msg_word_base", ctypes.c_int32),
         ("flat_max_words", ctypes.c_int32),
@@ -117,7 +115,7 @@ SIGNATURES = {
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
 }
 
-ABI_VERSION = 5   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 6   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

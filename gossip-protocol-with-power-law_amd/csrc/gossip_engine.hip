@@ -144,23 +144,36 @@ __global__ void k_stats_reduce(u64* __restrict__ partial, u64* __restrict__ stat
 
 // ---------------------------------------------------------------------------
 // expansion
+//
+// Message-List slots: vertex v's seen row lives in one of two
+// slot buffers S[0], S[1]; sp[v] says which (0xFF: none yet, reads as zero).
+// In round r the neighbours' rows are read from S[r & 1] and every receiver
+// writes its new seen row to S[(r + 1) & 1].  A sender u of round r received
+// in round r - 1 (or was injected in round r), so S[r & 1][u] is exactly
+// seen_r(u).  Reading u's whole Message-List instead of its frontier is exact:
+// every older bit of seen_r(u) was sent to all of u's live out-neighbours when
+// u first received it (forward-once), so a live receiver already holds it and
+// OR(...) & ~seen(v) is unchanged.  This drops the separate frontier rows: a
+// receiver writes one row per round instead of two.
 struct ExpandArgs {
   const int64_t* __restrict__ row_ptr;
   const int32_t* __restrict__ col;
-  const u64* __restrict__ front;       // frontier_r
-  const uint32_t* __restrict__ fpop;   // |frontier_r|
-  const u64* __restrict__ abits;       // bit v: frontier_r(v) != 0 (2 MB at 2^24; one word per 64 vertices)
-  const u64* __restrict__ sbits;       // bit v: frontier_r(v) is an id-list row (1 <= fpop <= list_max)
-  int32_t list_max;                    // frontier rows with <= list_max bits are id lists (0: none)
+  const u64* __restrict__ rows;        // S[r & 1]: seen rows of the round's senders
+  u64* slot[2];                        // S[0], S[1] (the receiver's own rows)
+  int32_t wslot;                       // (r + 1) & 1: the slot receivers write
+  uint8_t* __restrict__ sp;            // [n_alloc] slot of v's current seen row (0xFF: none)
+  uint8_t* __restrict__ ws;            // [n_alloc] bit p: slot p written this run
+  const uint32_t* __restrict__ fpop;   // |frontier_r|: bits received in round r - 1 (+ injected)
+  const u64* __restrict__ abits;       // bit v: fpop(v) != 0 (2 MB at 2^24)
   const int32_t* __restrict__ gcol;    // in-CSR columns in gather order (neighbour degree desc)
   const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
   int32_t early_exit;                  // this round scans with the coverage check
-  int32_t unfiltered;                  // read every in-neighbour row (inactive rows are zero)
+  int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
   const uint32_t* __restrict__ done_at;// |messages of v's component|: seenpop == done_at -> done
-  u64* __restrict__ next;
   uint32_t* __restrict__ fpop_next;
-  u64* __restrict__ seen;
+  u64* __restrict__ frx;               // exact frontier rows of round r (track_msg_forwards only)
+  u64* __restrict__ frx_next;          // exact frontier rows of round r + 1 (idem)
   uint32_t* __restrict__ seenpop;
   uint8_t* __restrict__ first;         // may be null
   u64* __restrict__ digest;            // may be null
@@ -187,15 +200,10 @@ struct ExpandArgs {
   int32_t wbase;                       // global word index of local word 0 (message shards)
   int32_t rr;                          // receipt round of this expansion (r + 1)
   int32_t hub_thr;
-  int32_t vpw;                         // vertices per wave (k_expand)
 };
 
-// Id-list frontier rows: a row with 1 <= fpop <= LIST_MAX new
-// bits holds its message ids as u16 in the first 64 B of its own row slot
-// (0xFFFF-padded) instead of the 8W-byte bitmap; the format is a pure function
-// of fpop, so no side array travels with the rows.  The gather ORs list rows
-// into a per-wave LDS row with ds_or_b64.  Only for W >= 16 (rows >= 128 B).
-constexpr int LIST_SLOTS = 32;   // u16 slots of one 64-byte list segment
+constexpr uint8_t SLOT_NONE = 0xFF;
+
 // occupancy target of k_expand (waves per SIMD; 0 = compiler's choice)
 #ifndef GP_EXPAND_WAVES
 #define GP_EXPAND_WAVES 0
@@ -205,80 +213,15 @@ constexpr int LIST_SLOTS = 32;   // u16 slots of one 64-byte list segment
 #else
 #define EXPAND_BOUNDS __launch_bounds__(BLOCK)
 #endif
-// EXPERIMENT: cache-policy bits of the gathered row loads (0 = compiler default)
-#ifndef GP_ROW_POLICY
-#define GP_ROW_POLICY 0
-#endif
-#if GP_ROW_POLICY == 1
-#define GP_ROW_POLICY_STR ""
-#elif GP_ROW_POLICY == 2
-#define GP_ROW_POLICY_STR "nt"
-#elif GP_ROW_POLICY == 3
-#define GP_ROW_POLICY_STR "sc1"
-#elif GP_ROW_POLICY == 4
-#define GP_ROW_POLICY_STR "sc0 sc1"
-#elif GP_ROW_POLICY == 5
-#define GP_ROW_POLICY_STR "sc1 nt"
-#elif GP_ROW_POLICY == 6
-#define GP_ROW_POLICY_STR "sc0 sc1 nt"
-#endif
 // rows each lane keeps in flight per gather step (MLP vs VGPRs)
 #ifndef GP_ROWS_IN_FLIGHT
 #define GP_ROWS_IN_FLIGHT 4
 #endif
-constexpr uint16_t SP_EMPTY = 0xFFFF;
-
-__device__ __forceinline__ bool is_list_row(uint32_t fp, int32_t list_max) {
-  return fp != 0u && fp <= (uint32_t)list_max;
-}
-
-// word `w` of row v (either format); for the rare paths (injection, push
-// staging, fixups, per-message sums) -- the gather has its own batched reader
-__device__ __forceinline__ u64 row_word(const u64* __restrict__ front, int64_t v, int words, uint32_t fp,
-                                        int32_t list_max, int w) {
-  if (fp == 0u) return 0ull;
-  if (is_list_row(fp, list_max)) {
-    const uint16_t* ids = reinterpret_cast<const uint16_t*>(front + (size_t)v * words);
-    u64 x = 0;
-#pragma unroll 4
-    for (int q = 0; q < LIST_SLOTS; ++q) {
-      const uint16_t id = ids[q];
-      if (id != SP_EMPTY && (int)(id >> 6) == w) x |= 1ull << (id & 63);
-    }
-    return x;
-  }
-  return front[(size_t)v * words + w];
-}
-
-// write the <= LIST_MAX ids staged in ids[0, tot) as the list segment of a row
-// slot: lanes 0..3 store 16 B (8 ids) each, 0xFFFF past tot
-__device__ __forceinline__ void store_list(u64* __restrict__ slot, const uint16_t* __restrict__ ids, uint32_t tot,
-                                           int lane) {
-  if (lane < 4) {
-    u64 p[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      u64 x = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t q = (uint32_t)(lane * 8 + h * 4 + k);
-        const u64 id = q < tot ? (u64)ids[q] : (u64)SP_EMPTY;
-        x |= id << (16 * k);
-      }
-      p[h] = x;
-    }
-    *reinterpret_cast<u64x2*>(slot + lane * 2) = u64x2{p[0], p[1]};
-  }
-}
 
 // per-wave LDS of the pull kernels
 struct WaveLds {
-  u64 acc[64];          // OR accumulator of id-list rows
   u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
-  int32_t idx[64];      // bitmap-row active neighbours of one pass
-  int32_t sidx[64];     // id-list-row active neighbours of one pass
-  uint16_t ids[64];     // id-list staging (finish_row)
-  uint32_t nids;        // id-list fill cursor
+  int32_t idx[64];      // active neighbours of one pass
 };
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -297,6 +240,12 @@ __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t x, int lane) {
   return inc - x;
 }
 
+__device__ __forceinline__ u64 wave_sum_u64(u64 x) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) x += __shfl_xor(x, s);
+  return x;
+}
+
 // OR-reduce the row slots of the wave: afterwards every lane holds the full
 // result for its lw column.
 template <int W>
@@ -309,105 +258,38 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
   }
 }
 
-// scan modes of a pull round (compile-time, so each variant keeps only the
-// registers it needs): the per-arc activity probe, plus id-list rows, or no
-// probe at all (unfiltered dense rounds)
-enum ScanMode { SCAN_FILTERED = 0, SCAN_LISTS = 1, SCAN_UNFILTERED = 2 };
+// scan modes of a pull round (compile-time): the per-arc activity probe, or no
+// probe at all (unfiltered dense rounds: the bitmap misses L2 under the row stream)
+enum ScanMode { SCAN_FILTERED = 0, SCAN_UNFILTERED = 2 };
 
-// classify neighbour u for the round: u (bitmap row), -(u + 2) (id-list row),
-// -1 (inactive: its row is never read).  Split in two so the probe load can be
-// issued a vertex ahead of its use (k_expand's pipeline): probe_raw issues the
-// bitmap load, classify decodes it.
+// neighbour u if its row is read this round, else -1
 template <int MODE>
-__device__ __forceinline__ u64x2 probe_raw(const ExpandArgs& a, int32_t u) {
-  if constexpr (MODE == SCAN_UNFILTERED) {   // dense round: no bitmap probe (it misses L2 under the row stream)
-    return u64x2{0, 0};
-  } else if constexpr (MODE == SCAN_LISTS) {  // one 16-byte probe: activity + list format
-    return u64x2{a.abits[u >> 6], a.sbits[u >> 6]};
-  } else {
-    return u64x2{a.abits[u >> 6], 0};
-  }
-}
-template <int MODE>
-__device__ __forceinline__ int32_t classify(u64x2 pb, int32_t u) {
+__device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
   if constexpr (MODE == SCAN_UNFILTERED) {
     return u;
   } else {
-    if (!((pb.x >> (u & 63)) & 1ull)) return -1;
-    if constexpr (MODE == SCAN_LISTS) return ((pb.y >> (u & 63)) & 1ull) ? -(u + 2) : u;
-    return u;
+    return ((a.abits[u >> 6] >> (u & 63)) & 1ull) ? u : -1;
   }
 }
-template <int MODE>
-__device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
-  return classify<MODE>(probe_raw<MODE>(a, u), u);
-}
 
-// OR the staged rows of one pass into acc: id lists (L.sidx[0, scnt)) through
-// the LDS row, bitmap rows (L.idx[0, cnt)) into registers, GP_ROWS_IN_FLIGHT
+// OR the staged rows of one pass (L.idx[0, cnt)) into acc, GP_ROWS_IN_FLIGHT
 // wave-instructions of 16 B per lane in flight.  Early exit (bottom-up,
 // Beamer et al. SC'12): with `ee` the wave stops once acc | seen covers every
 // message of the vertex's component (want = cm & ~seen, group-0 lanes); OR is
 // idempotent, so acc & ~seen is exactly what the full scan would give.
 // Returns true on early exit.
-template <int W, bool LISTS>
-__device__ __forceinline__ bool gather_rows(const ExpandArgs& a, WaveLds& L, int cnt, int scnt, int lane, int g,
-                                            int lw, u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
+template <int W>
+__device__ __forceinline__ bool gather_rows(const ExpandArgs& a, WaveLds& L, int cnt, int g, int lw, u64x2& acc,
+                                            WaveStats& st, bool ee, u64x2 want) {
   constexpr int RPI = Geo<W>::RPI;
-  constexpr int WPL = Geo<W>::WPL;
-  if constexpr (LISTS && W >= 16) {
-    if (scnt) {
-      if (lane < W) L.acc[lane] = 0ull;
-      wave_sync_lds();
-      // 8 lanes per 64-byte list (8 B = 4 ids each), 8 lists per
-      // wave-instruction, LQ instructions in flight before the first LDS OR
-      constexpr int LQ = 4;
-      for (int k0 = 0; k0 < scnt; k0 += 8 * LQ) {
-        u64 r[LQ];
-#pragma unroll
-        for (int q = 0; q < LQ; ++q) {
-          const int k = k0 + q * 8 + (lane >> 3);
-          r[q] = ~0ull;
-          if (k < scnt) r[q] = a.front[(size_t)L.sidx[k] * W + (lane & 7)];
-        }
-#pragma unroll
-        for (int q = 0; q < LQ; ++q) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t id = (uint32_t)(r[q] >> (16 * k)) & 0xFFFFu;
-            if (id != SP_EMPTY) atomicOr(&L.acc[id >> 6], 1ull << (id & 63));
-          }
-        }
-      }
-      wave_sync_lds();
-      if (g == 0) {
-        acc.x |= L.acc[lw * WPL];
-        if constexpr (WPL == 2) acc.y |= L.acc[lw * WPL + 1];
-      }
-      st.add(S_GATHERED, scnt);
-      st.add(S_SP_GATHERED, scnt);
-    }
-  }
   for (int k0 = 0; k0 < cnt; k0 += GP_ROWS_IN_FLIGHT * RPI) {
     u64x2 r[GP_ROWS_IN_FLIGHT];
 #pragma unroll
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
       const int k = k0 + g + q * RPI;
       r[q] = u64x2{0, 0};
-#if GP_ROW_POLICY != 0
-      if constexpr (W >= 2) {   // EXPERIMENT: cache-policy bits on the row loads
-        if (k < cnt) {
-          const u64* p = a.front + (size_t)L.idx[k] * W + lw * 2;
-          asm volatile("global_load_dwordx4 %0, %1, off " GP_ROW_POLICY_STR : "+v"(r[q]) : "v"(p) : "memory");
-        }
-        continue;
-      }
-#endif
-      if (k < cnt) r[q] = load_piece<W>(a.front, L.idx[k], lw);
+      if (k < cnt) r[q] = load_piece<W>(a.rows, L.idx[k], lw);
     }
-#if GP_ROW_POLICY != 0
-    if constexpr (W >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
 #pragma unroll
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
     st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
@@ -422,29 +304,30 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, WaveLds& L, int
   return false;
 }
 
-// stage one pass of classified neighbours (e: this lane's entry) in LDS;
-// returns the counts through cnt / scnt
-__device__ __forceinline__ void stage_pass(WaveLds& L, int32_t e, int lane, int& cnt, int& scnt) {
-  const u64 dmask = __ballot(e >= 0);
-  const u64 smask = __ballot(e < -1);
-  cnt = __popcll(dmask);
-  scnt = __popcll(smask);
-  if (e >= 0) L.idx[lane_rank(dmask)] = e;
-  if (e < -1) L.sidx[lane_rank(smask)] = -(e + 2);
+// stage one pass of probed neighbours (e: this lane's entry, -1 = none) in
+// LDS; returns their count
+__device__ __forceinline__ int stage_pass(WaveLds& L, int32_t e) {
+  const u64 m = __ballot(e >= 0);
+  if (e >= 0) L.idx[lane_rank(m)] = e;
   wave_sync_lds();
+  return __popcll(m);
+}
+
+// the receiver's current seen row, piece lw (slot sv_slot; SLOT_NONE: empty)
+template <int W>
+__device__ __forceinline__ u64x2 load_seen(const ExpandArgs& a, int v, uint32_t sv_slot, int lw) {
+  return sv_slot != SLOT_NONE ? load_piece<W>(a.slot[sv_slot], v, lw) : u64x2{0, 0};
 }
 
 // early exit: park the receiver's seen row in LDS (finish_row reuses it) and
 // return, in group-0 lanes, the messages of its component it still lacks
-// (spop == 0: the row was never written this run and reads as zero -- reset
-// does not clear the Message-Lists)
 template <int W>
-__device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, int64_t i, WaveLds& L, int g,
-                                                   int lw, uint32_t spop) {
+__device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, WaveLds& L, int g, int lw,
+                                                   uint32_t sv_slot) {
   constexpr int WPL = Geo<W>::WPL;
   u64x2 want = {0, 0};
   if (g == 0) {
-    const u64x2 sv = spop ? load_piece<W>(a.seen, i, lw) : u64x2{0, 0};
+    const u64x2 sv = load_seen<W>(a, v, sv_slot, lw);
     const u64x2 cm = load_piece<W>(a.cmask, a.midx[v], lw);
     L.seen[lw * WPL] = sv.x;
     if constexpr (WPL == 2) L.seen[lw * WPL + 1] = sv.y;
@@ -463,10 +346,9 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
     int32_t ent = -1;
     if (lane < n) ent = probe<MODE>(a, a.gcol[j0 + lane]);
     st.add(S_ARCS, n);
-    int cnt, scnt;
-    stage_pass(L, ent, lane, cnt, scnt);
-    if (cnt + scnt == 0) continue;
-    const bool stop = gather_rows<W, MODE == SCAN_LISTS>(a, L, cnt, scnt, lane, g, lw, acc, st, ee, want);
+    const int cnt = stage_pass(L, ent);
+    if (cnt == 0) continue;
+    const bool stop = gather_rows<W>(a, L, cnt, g, lw, acc, st, ee, want);
     wave_sync_lds();
     if (stop) break;
   }
@@ -491,27 +373,27 @@ __device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int w
   }
 }
 
-// receiver side of vertex v (local index i): apply seen, write next, counters.
-// have_sv: the seen row is parked in L.seen (early exit), else it is loaded
-// here -- unless spop (|seen(v)|) is 0: a row never written this run reads as
-// zero (reset does not clear the Message-Lists).
+// receiver side of vertex v (local index i): new = acc & ~seen; write the new
+// seen row to slot wslot, counters.  have_sv: the seen row is parked in L.seen
+// (early exit), else it is loaded here from slot sv_slot.
 template <int W>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
-                                           int g, int lw, WaveStats& st, WaveLds& L, bool have_sv, uint32_t spop) {
+                                           int g, int lw, WaveStats& st, WaveLds& L, bool have_sv,
+                                           uint32_t sv_slot) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
     if (lane == 0) a.fpop_next[v] = 0;
     return;
   }
-  if (!have_sv && spop) st.add(S_SEEN_READ, 1);
+  if (!have_sv && sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
   u64x2 sv = {0, 0}, nw = {0, 0};
   if (g == 0) {
     if (have_sv) {
       sv.x = L.seen[lw * WPL];
       if constexpr (WPL == 2) sv.y = L.seen[lw * WPL + 1];
-    } else if (spop) {
-      sv = load_piece<W>(a.seen, i, lw);
+    } else {
+      sv = load_seen<W>(a, v, sv_slot, lw);
     }
     nw = acc & ~sv;
   }
@@ -521,37 +403,9 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
     if (lane == 0) a.fpop_next[v] = 0;
     return;
   }
-  const bool as_ids = W >= 16 && tot <= (uint32_t)a.list_max;
-  if (as_ids) {   // compact the <= LIST_MAX new bits into a 64-byte id list (order is immaterial)
-    if (lane == 0) L.nids = 0;
-    wave_sync_lds();
-    uint32_t off = 0;
-    if (pc) off = atomicAdd(&L.nids, pc);
-    if (g == 0) {
-      u64 x = nw.x;
-      while (x) {
-        const int bb = __ffsll((long long)x) - 1;
-        x &= x - 1;
-        L.ids[off++] = (uint16_t)((lw * WPL) * 64 + bb);
-      }
-      if constexpr (WPL == 2) {
-        x = nw.y;
-        while (x) {
-          const int bb = __ffsll((long long)x) - 1;
-          x &= x - 1;
-          L.ids[off++] = (uint16_t)((lw * WPL + 1) * 64 + bb);
-        }
-      }
-    }
-    wave_sync_lds();
-    store_list(a.next + (size_t)v * W, L.ids, tot, lane);
-    wave_sync_lds();
-    st.add(S_SP_WRITTEN, 1);
-  }
   if (g == 0) {
-    if (!as_ids) store_piece<W>(a.next, v, lw, nw);
-    // a row first written this run is written whole (its stale pieces go)
-    if ((nw.x | nw.y) || spop == 0) store_piece<W>(a.seen, i, lw, sv | nw);
+    store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);   // the whole row: the slot may hold an older one
+    if (a.frx_next) store_piece<W>(a.frx_next, v, lw, nw);
     if (a.first) {
       uint8_t* row = a.first + (size_t)i * (W * 64);
       if (nw.x) set_first_bytes(row, lw * WPL, nw.x, (uint32_t)a.rr);
@@ -570,6 +424,8 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   if (lane == 0) {
     a.fpop_next[v] = tot;
     a.seenpop[i] += tot;
+    a.sp[v] = (uint8_t)a.wslot;
+    a.ws[v] |= (uint8_t)(1u << a.wslot);
   }
   st.add(S_NEW_BITS, tot);
   st.add(S_RECEIVERS, 1);
@@ -577,17 +433,11 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   st.add(S_NEXT_ARCS, (u64)(uint32_t)max(a.deg_live[v], 0));
 }
 
-__device__ __forceinline__ u64 wave_sum_u64(u64 x) {
-#pragma unroll
-  for (int s = 32; s > 0; s >>= 1) x += __shfl_xor(x, s);
-  return x;
-}
-
 // main pull kernel: a wave owns 64 consecutive vertices.  The per-vertex
 // checks (sender accounting, down / done / hub / no in-arcs) run lane-parallel
 // with coalesced loads; the wave then scans, one receiver at a time, only the
-// vertices that can still receive something.  Kept lean on registers (72
-// VGPRs, 7 waves per SIMD): the dense rounds are bound by the rows in flight.
+// vertices that can still receive something.  Kept lean on registers (7 waves
+// per SIMD): the dense rounds are bound by the rows in flight.
 template <int W, int MODE>
 __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
@@ -603,7 +453,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     const int64_t li = base + lane;
     bool need = false, act = false;
     u64 sends = 0;
-    uint32_t sp = 0;
+    uint32_t slot_of = SLOT_NONE;
     if (li < a.nloc) {
       const int v = (int)(a.vbegin + li);
       const uint32_t fp = a.fpop[v];
@@ -611,9 +461,9 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
       const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
-      sp = a.seenpop[li];
-      need = !(a.state[v] & ST_DOWN) && sp < a.done_at[v] && !hub && e > b;
+      need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
       if (!need && !hub) a.fpop_next[v] = 0;
+      slot_of = a.sp[v];
     }
     st.add(S_SENDS, wave_sum_u64(sends));
     st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
@@ -626,15 +476,15 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       const int64_t i = base + k;
       const int v = uniform((int)(a.vbegin + i));
       const int64_t vb = a.row_ptr[v], ve = a.row_ptr[v + 1];   // scalar loads
-      const uint32_t spop = (uint32_t)__builtin_amdgcn_readlane((int)sp, k);
+      const uint32_t sv_slot = (uint32_t)__builtin_amdgcn_readlane((int)slot_of, k);
       u64x2 acc = {0, 0}, want = {0, 0};
       if (ee) {
-        if (spop) st.add(S_SEEN_READ, 1);
-        want = early_exit_target<W>(a, v, i, L, g, lw, spop);
+        if (sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
+        want = early_exit_target<W>(a, v, L, g, lw, sv_slot);
       }
       gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
-      finish_row<W>(a, v, i, acc, lane, g, lw, st, L, ee, spop);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot);
     }
   }
   flush_stats(st, a.partial);
@@ -649,8 +499,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
 // active rows are gathered RPI per wave-instruction whatever receiver they
 // belong to, and OR-ed into per-receiver accumulators in LDS (ds_or_b64).  The
 // receiver side then runs lane-parallel, one receiver per lane.  No early exit
-// (narrow rows are cheap next to the arc scan); id-list rows are not read here
-// (the per-receiver kernel takes rounds that may hold them).
+// (narrow rows are cheap next to the arc scan).
 constexpr int FLAT_CAP = 512;   // arc positions per owner window
 // row wave-instructions in flight per lane (VGPRs vs occupancy: 2 -> 66 VGPRs at W = 8)
 #ifndef GP_FLAT_ROWS_IN_FLIGHT
@@ -682,7 +531,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
     const int64_t li = base + lane;
     bool need = false, act = false;
     u64 sends = 0;
-    uint32_t sp = 0, deg = 0;
+    uint32_t spop = 0, deg = 0, slot_of = SLOT_NONE;
     int64_t vb = 0;
     int v = 0;
     if (li < a.nloc) {
@@ -693,10 +542,11 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       vb = a.row_ptr[v];
       const int64_t e = a.row_ptr[v + 1];
       const bool hub = e - vb > a.hub_thr;   // split over waves by the hub kernels
-      sp = a.seenpop[li];
-      need = !(a.state[v] & ST_DOWN) && sp < a.done_at[v] && !hub && e > vb;
+      spop = a.seenpop[li];
+      need = !(a.state[v] & ST_DOWN) && spop < a.done_at[v] && !hub && e > vb;
       if (!need && !hub) a.fpop_next[v] = 0;
       deg = (uint32_t)(e - vb);
+      slot_of = a.sp[v];
     }
     st.add(S_SENDS, wave_sum_u64(sends));
     st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
@@ -763,16 +613,16 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
           col[q] = -1;
           if (p < wn) col[q] = a.gcol[b + (g0 + p - s)];
         }
-        u64 raw[QA];   // activity words (no list rows in this kernel)
+        u64 raw[QA];   // activity words, all in flight before the first use
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
-          raw[q] = 0;
+          raw[q] = ~0ull;
           if constexpr (MODE != SCAN_UNFILTERED)
             if (col[q] >= 0) raw[q] = a.abits[col[q] >> 6];
         }
 #pragma unroll
         for (int q = 0; q < QA; ++q) {
-          const int32_t u = col[q] >= 0 ? classify<MODE>(u64x2{raw[q], 0}, col[q]) : -1;
+          const int32_t u = (col[q] >= 0 && ((raw[q] >> (col[q] & 63)) & 1ull)) ? col[q] : -1;
           const u64 am = __ballot(u >= 0);
           const int cnt = __popcll(am);
           if (cnt == 0) continue;
@@ -789,7 +639,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
             for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
               const int k = k0 + g + t * RPI;
               r[t] = u64x2{0, 0};
-              if (k < cnt) r[t] = load_piece<W>(a.front, F.idx[k], lw);
+              if (k < cnt) r[t] = load_piece<W>(a.rows, F.idx[k], lw);
             }
 #pragma unroll
             for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
@@ -808,7 +658,8 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       }
     }
     st.add(S_GATHERED, gathered);
-    // receiver side, one receiver per lane
+    // receiver side, one receiver per lane: two passes over the row (count,
+    // then write) so that a receiver with nothing new writes nothing
     u64 nbits = 0, nrecv = 0, nwritten = 0, narcs = 0, nseen = 0;
     if (need) {
       u64 any = 0;
@@ -817,27 +668,36 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       if (!any) {
         a.fpop_next[v] = 0;
       } else {
-        if (sp) nseen = 1;
+        const u64* __restrict__ srow = slot_of != SLOT_NONE ? a.slot[slot_of] + (size_t)v * W : nullptr;
+        if (srow) nseen = 1;
         uint32_t tot = 0;
-        u64 dig = 0;
-        u64* __restrict__ nrow = a.next + (size_t)v * W;
-        u64* __restrict__ srow = a.seen + (size_t)li * W;
-        uint8_t* __restrict__ frow = a.first ? a.first + (size_t)li * (W * 64) : nullptr;
-#pragma unroll 2
+#pragma unroll 4
         for (int w = 0; w < W; ++w) {
-          const u64 s = sp ? srow[w] : 0ull;
+          const u64 s = srow ? srow[w] : 0ull;
           const u64 nw = F.acc[lane][w] & ~s;
-          nrow[w] = nw;
-          if (nw || !sp) srow[w] = s | nw;   // a row first written this run is written whole
-          if (nw) {
-            tot += (uint32_t)__popcll(nw);
-            if (a.digest) dig ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + w), nw);
-            if (frow) set_first_bytes(frow, w, nw, (uint32_t)a.rr);
-          }
+          F.acc[lane][w] = nw;
+          tot += (uint32_t)__popcll(nw);
         }
         a.fpop_next[v] = tot;
         if (tot) {
-          a.seenpop[li] = sp + tot;
+          u64 dig = 0;
+          u64* __restrict__ drow = a.slot[a.wslot] + (size_t)v * W;
+          u64* __restrict__ xrow = a.frx_next ? a.frx_next + (size_t)v * W : nullptr;
+          uint8_t* __restrict__ frow = a.first ? a.first + (size_t)li * (W * 64) : nullptr;
+#pragma unroll 2
+          for (int w = 0; w < W; ++w) {
+            const u64 nw = F.acc[lane][w];
+            const u64 s = srow ? srow[w] : 0ull;   // srow may be drow (in place): read first
+            drow[w] = s | nw;
+            if (xrow) xrow[w] = nw;
+            if (nw) {
+              if (a.digest) dig ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + w), nw);
+              if (frow) set_first_bytes(frow, w, nw, (uint32_t)a.rr);
+            }
+          }
+          a.seenpop[li] = spop + tot;
+          a.sp[v] = (uint8_t)a.wslot;
+          a.ws[v] |= (uint8_t)(1u << a.wslot);
           if (a.digest) a.digest[li] ^= dig;
           nbits = tot;
           nrecv = 1;
@@ -870,11 +730,10 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
     const HubItem h = a.hub_items[it];
     const int64_t i = h.v - a.vbegin;
     u64x2 acc = {0, 0};
-    const uint32_t spop = a.seenpop[i];
-    if (!(a.state[h.v] & ST_DOWN) && spop < a.done_at[h.v]) {
+    if (!(a.state[h.v] & ST_DOWN) && a.seenpop[i] < a.done_at[h.v]) {
       const bool ee = a.early_exit != 0;
       u64x2 want = {0, 0};
-      if (ee) want = early_exit_target<W>(a, h.v, i, s_w[wib], g, lw, spop);
+      if (ee) want = early_exit_target<W>(a, h.v, s_w[wib], g, lw, a.sp[h.v]);
       gather_scan<W, MODE>(a, h.beg, h.end, s_w[wib], lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
     }
@@ -899,8 +758,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
   if (h < a.n_items) {
     const int v = a.hubs[h];
     const int64_t i = v - a.vbegin;
-    const uint32_t spop = a.seenpop[i];
-    if ((a.state[v] & ST_DOWN) || spop >= a.done_at[v]) {
+    if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= a.done_at[v]) {
       if (lane == 0) a.fpop_next[v] = 0;
     } else {
       st.add(S_VISITED, 1);
@@ -910,7 +768,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
         for (int p = p0; p < p1; ++p)
           if (a.hub_pnz[p]) acc |= load_piece<W>(a.hub_partial, p, lw);
       }
-      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, spop);
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
     }
   }
   flush_stats(st, a.partial);
@@ -918,11 +776,14 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
 
 // ---------------------------------------------------------------------------
 // push mode for sparse rounds (direction-optimising, Beamer et al. SC'12):
-// every active sender ORs the NON-ZERO words of its frontier row into the
-// accumulator rows of its live out-neighbours (64-bit atomicOr, order-free so
-// bit-exact) and sets the receiver's bit in `tbits` (fire-and-forget atomicOr
-// on a 2 MB bitmap); k_touch_list compacts the bitmap and k_apply runs the same
-// receiver side as the pull (finish_row) and re-zeroes acc.
+// every active sender ORs the NON-ZERO words of its row into the accumulator
+// rows of its live out-neighbours (64-bit atomicOr, order-free so bit-exact)
+// and sets the receiver's bit in `tbits` (fire-and-forget atomicOr on a 2 MB
+// bitmap); k_touch_list compacts the bitmap and k_apply runs the same receiver
+// side as the pull (finish_row) and re-zeroes acc.  The sender row is its
+// whole Message-List S[r & 1][u] (a superset of its frontier whose extra bits
+// every live out-neighbour already holds, see ExpandArgs), or the exact
+// frontier row when track_msg_forwards keeps those.
 
 // active senders from the bitmap: one thread per 64-vertex word, block-level
 // compaction, one cursor add per block; big senders go to their own list
@@ -1017,26 +878,11 @@ template <int W>
 __device__ __forceinline__ int stage_row(const ExpandArgs& a, int32_t u, u64* __restrict__ srow,
                                          int8_t* __restrict__ swords, int lane) {
   u64 x = 0;
-  const uint32_t fp = a.fpop[u];
-  if (W >= 16 && is_list_row(fp, a.list_max)) {   // id-list row: rebuild the words through LDS
-    if (lane < W) srow[lane] = 0ull;
-    wave_sync_lds();
-    if (lane < LIST_SLOTS) {
-      const uint16_t id = reinterpret_cast<const uint16_t*>(a.front + (size_t)u * W)[lane];
-      if (id != SP_EMPTY) atomicOr(&srow[id >> 6], 1ull << (id & 63));
-    }
-    wave_sync_lds();
-    if (lane < W) x = srow[lane];
-    wave_sync_lds();
-  } else if (lane < W) {
-    x = a.front[(size_t)u * W + lane];
-  }
+  if (lane < W) x = a.frx ? a.frx[(size_t)u * W + lane] : a.rows[(size_t)u * W + lane];
   const u64 nzm = __ballot(x != 0ull);
   if (lane < W) srow[lane] = x;
   if (x) swords[lane_rank(nzm)] = (int8_t)lane;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wave_sync_lds();
   return __popcll(nzm);
 }
 
@@ -1064,7 +910,6 @@ __global__ __launch_bounds__(BLOCK) void k_push(ExpandArgs a) {
     const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
     const int64_t jb = a.orp[u], je = a.orp[u + 1];
     st.add(S_GATHERED, 1);
-    if (W >= 16 && is_list_row(a.fpop[u], a.list_max)) st.add(S_SP_GATHERED, 1);
     st.add(S_ARCS, (u64)(je - jb));
     st.add(S_ATOMICS, (u64)(je - jb) * (u64)nnz);
     push_arcs<W>(a, jb, je, s_row[wib], s_words[wib], nnz, lane);
@@ -1130,51 +975,43 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
       store_piece<W>(a.acc, v, lw, u64x2{0, 0});
     }
     st.add(S_VISITED, 1);
-    finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.seenpop[i]);
+    finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
   }
   flush_stats(st, a.partial);
 }
 
-// frontier bitmaps, interleaved per 64 vertices so one 16-byte probe answers
-// both questions: .x bit = (fpop != 0), .y bit = id-list row (1 <= fpop <= list_max)
-__global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, int32_t list_max,
-                                                  u64* __restrict__ abits, u64* __restrict__ sbits,
+// frontier activity bitmap: bit v = (fpop[v] != 0), one word per 64 vertices
+__global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, u64* __restrict__ abits,
                                                   int64_t n) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
     const int64_t v = v0 + lane;
-    const uint32_t fp = v < n ? fpop[v] : 0u;
-    const u64 m = __ballot(fp != 0u);
-    const u64 sm = __ballot(is_list_row(fp, list_max));
-    if (lane == 0) {
-      abits[v0 >> 6] = m;
-      sbits[v0 >> 6] = sm;
-    }
+    const u64 m = __ballot(v < n && fpop[v] != 0u);
+    if (lane == 0) abits[v0 >> 6] = m;
   }
 }
 
-// unfiltered rounds: make every frontier row readable without
-// the activity check -- rows of inactive vertices (fpop == 0: never written,
-// or crashed) become zero, id-list rows are expanded to bitmap rows.  One wave
-// per 64-vertex bitmap word; fully active dense words cost one load.
+// unfiltered rounds: every in-neighbour row of S[r & 1] is
+// read, so each must be a subset of its vertex's Message-List -- true for
+// every row written this run (seen rows only grow).  Rows of inactive vertices
+// whose slot was not written this run hold data of an earlier run: zero them.
+// One wave per 64-vertex bitmap word; fully active words cost two loads.
+// (Only without liveness: a crashed vertex may hold bits it never sent.)
 template <int W>
-__global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64* __restrict__ abits, const u64* __restrict__ sbits,
-                                                      const uint32_t* __restrict__ fpop, int32_t list_max,
-                                                      u64* __restrict__ front, int64_t n_alloc) {
+__global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64* __restrict__ abits, uint8_t* __restrict__ ws,
+                                                      u64* __restrict__ rows, int32_t rslot, int64_t n_alloc) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
   if (w * 64 >= n_alloc) return;
-  const u64x2 pb = u64x2{abits[w], sbits[w]};
-  u64 todo = ~pb.x | pb.y;
+  const int64_t v0 = w * 64 + lane;
+  const bool stale = v0 < n_alloc && !((abits[w] >> lane) & 1ull) && !((ws[v0] >> rslot) & 1u);
+  u64 todo = __ballot(stale);
+  if (stale) ws[v0] |= (uint8_t)(1u << rslot);
   while (todo) {
     const int b = __ffsll((long long)todo) - 1;
     todo &= todo - 1;
-    const int64_t v = w * 64 + b;
-    if (v >= n_alloc) break;
-    const u64 x = ((pb.y >> b) & 1ull) ? row_word(front, v, W, fpop[v], list_max, lane) : 0ull;
-    __builtin_amdgcn_wave_barrier();   // every lane has read the list before it is overwritten
-    if (lane < W) front[(size_t)v * W + lane] = x;
+    if (lane < W) rows[(size_t)(w * 64 + b) * W + lane] = 0ull;
   }
 }
 
@@ -1237,17 +1074,21 @@ __global__ void k_done_at(const int32_t* __restrict__ comp, const uint32_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// injection (I_r): one wave per (round, origin) group.  Frontier rows are
-// replicated on every rank, so every rank applies every group; the owner of
-// the origin also updates its Message-List, first-receipt and counters.
+// injection (I_r): one wave per (round, origin) group.  The origin's seen row
+// is copied into slot r & 1 with the new messages (so that it is read as a
+// sender this round, see ExpandArgs) and its frontier count grows.  Slots and
+// popcounts are replicated on every rank, so every rank applies every group;
+// the owner of the origin also updates seenpop, first-receipt and counters.
 struct InjectArgs {
-  int32_t list_max;                    // id-list rows (0: none)
   const int32_t* __restrict__ origin;
   const u64* __restrict__ bits;
   const uint32_t* __restrict__ cnt;
-  u64* __restrict__ front;
+  u64* slot[2];
+  int32_t rslot;                       // r & 1
+  uint8_t* __restrict__ sp;
+  uint8_t* __restrict__ ws;
   uint32_t* __restrict__ fpop;
-  u64* __restrict__ seen;
+  u64* __restrict__ frx;               // exact frontier rows (track_msg_forwards only)
   uint32_t* __restrict__ seenpop;
   uint8_t* __restrict__ first;
   u64* __restrict__ digest;
@@ -1273,38 +1114,29 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
     if (a.state[o] & ST_DOWN) {
       if (owned) st.add(S_LOST, a.cnt[gi]);
     } else {
-      __shared__ uint16_t s_ids[WAVES][LIST_SLOTS];
+      const uint32_t cur = a.sp[o];
       const uint32_t fp = a.fpop[o];
-      u64 b = 0, f = 0;
+      u64 b = 0, s = 0, f = 0;
       if (lane < a.words) {
         b = a.bits[gi * a.words + lane];
-        f = row_word(a.front, o, a.words, fp, a.list_max, lane) | b;
+        if (cur != SLOT_NONE) s = a.slot[cur][(size_t)o * a.words + lane];
+        if (a.frx && fp) f = a.frx[(size_t)o * a.words + lane];
       }
-      const uint32_t pc = (uint32_t)__popcll(f);
-      const uint32_t tot = wave_sum_u32(pc);
-      __builtin_amdgcn_wave_barrier();   // the old row is read before it is rewritten
-      if (a.words >= 16 && tot <= (uint32_t)a.list_max) {   // still small: id list
-        uint32_t off = wave_excl_scan_u32(pc, lane);
-        u64 x = f;
-        while (x) {
-          const int bb = __ffsll((long long)x) - 1;
-          x &= x - 1;
-          s_ids[wib][off++] = (uint16_t)(lane * 64 + bb);
-        }
-        wave_sync_lds();
-        store_list(a.front + (size_t)o * a.words, s_ids[wib], tot, lane);
-      } else if (lane < a.words) {
-        a.front[(size_t)o * a.words + lane] = f;
+      __builtin_amdgcn_wave_barrier();   // the old rows are read before they are rewritten
+      if (lane < a.words) {
+        a.slot[a.rslot][(size_t)o * a.words + lane] = s | b;
+        if (a.frx) a.frx[(size_t)o * a.words + lane] = f | b;
       }
-      if (lane == 0) a.fpop[o] = tot;
+      const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
+      if (lane == 0) {
+        a.fpop[o] = fp + nb;
+        a.sp[o] = (uint8_t)a.rslot;
+        a.ws[o] |= (uint8_t)(1u << a.rslot);
+      }
       if (owned) {
         const int64_t i = o - a.vbegin;
-        const uint32_t sp0 = a.seenpop[i];   // 0: the row is stale from an earlier run
-        if (lane < a.words) {
-          a.seen[i * a.words + lane] = (sp0 ? a.seen[i * a.words + lane] : 0ull) | b;
-          if (a.first && b) set_first_bytes(a.first + (size_t)i * a.words * 64, lane, b, (uint32_t)a.r);
-        }
-        const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
+        if (lane < a.words && a.first && b)
+          set_first_bytes(a.first + (size_t)i * a.words * 64, lane, b, (uint32_t)a.r);
         if (a.digest) {
           u64 t = b ? digest_term((uint32_t)a.r, (uint32_t)(a.wbase + lane) | DIGEST_INJECT, b) : 0ull;
           t = wave_xor_u64(t);
@@ -1439,9 +1271,10 @@ __global__ __launch_bounds__(BLOCK) void k_detect(LiveArgs a) {
 // over rows [0, count).  Lane l holds word l % W of vertex slot l / W; each lane
 // keeps 64 register counters per output.
 struct BitsumArgs {
-  const u64* __restrict__ rows;       // [count][W]
-  const uint32_t* __restrict__ guard; // optional: frontier popcounts (row valid iff != 0; format)
-  int32_t list_max;                   // with guard: rows with guard <= list_max are id lists
+  const u64* __restrict__ rows;       // [count][W] (when sel is null)
+  const uint32_t* __restrict__ guard; // optional: row valid iff guard[i] != 0
+  const u64* slot[2];                 // with sel: row i is slot[sel[i]][i] (SLOT_NONE: zero)
+  const uint8_t* __restrict__ sel;
   const int32_t* __restrict__ weight; // [count]
   u64* __restrict__ cnt;              // [W*64] or null
   u64* __restrict__ wsum;             // [W*64] or null
@@ -1470,8 +1303,12 @@ __global__ __launch_bounds__(BLOCK) void k_bitsum(BitsumArgs a) {
   const int64_t step = (int64_t)gridDim.x * WAVES * VPS;
   for (int64_t i = ((int64_t)blockIdx.x * WAVES + wib) * VPS + q; i < a.count; i += step) {
     u64 x = 0;
-    if (!a.guard) x = a.rows[i * W + w];
-    else x = row_word(a.rows, i, W, a.guard[i], a.list_max, w);
+    if (a.sel) {
+      const uint32_t p = a.sel[i];
+      if (p != SLOT_NONE) x = a.slot[p][i * W + w];
+    } else if (!a.guard || a.guard[i] != 0) {
+      x = a.rows[i * W + w];
+    }
     const uint32_t wt = SUM ? (uint32_t)max(a.weight[i], 0) : 0u;
 #pragma unroll
     for (int b = 0; b < 64; ++b) {
@@ -1520,19 +1357,22 @@ static int grid_for(int64_t work, int64_t per_block) {
 static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.row_ptr = c->d_row_ptr;
   a.col = c->d_col;
-  a.front = c->d_front[c->cur];
+  a.rows = c->d_slot[c->cur];
+  a.slot[0] = c->d_slot[0];
+  a.slot[1] = c->d_slot[1];
+  a.wslot = c->cur ^ 1;
+  a.sp = c->d_sp;
+  a.ws = c->d_ws;
   a.fpop = c->d_fpop[c->cur];
   a.abits = c->d_abits;
-  a.sbits = c->d_sbits;
-  a.list_max = c->list_max();
+  a.frx = c->d_frx[0] ? c->d_frx[c->cur] : nullptr;
+  a.frx_next = c->d_frx[0] ? c->d_frx[c->cur ^ 1] : nullptr;
   a.done_at = c->d_done_at;
   a.gcol = c->d_gcol;
   a.midx = c->d_midx;
   a.cmask = c->d_cmask;
   a.early_exit = c->early_exit_now ? 1 : 0;
-  a.next = c->d_front[c->cur ^ 1];
   a.fpop_next = c->d_fpop[c->cur ^ 1];
-  a.seen = c->d_seen;
   a.seenpop = c->d_seenpop;
   a.first = c->cfg.track_first ? c->d_first : nullptr;
   a.digest = c->cfg.track_digest ? c->d_digest : nullptr;
@@ -1550,7 +1390,6 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.wbase = c->cfg.msg_word_base;
   a.rr = c->round + 1;
   a.hub_thr = c->cfg.hub_threshold;
-  a.vpw = 4;
   a.orp = c->directed ? c->d_out_row_ptr : c->d_row_ptr;
   a.ocol = c->directed ? c->d_out_col : c->d_col;
   a.acc = c->d_acc;
@@ -1583,13 +1422,10 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   const int64_t per_block = (int64_t)WAVES * 64;
   if (a.unfiltered)
     hipLaunchKernelGGL(k_fixup_rows<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
-                       c->d_abits, c->d_sbits, c->d_fpop[c->cur], a.list_max, c->d_front[c->cur], c->n_alloc);
-  // id-list rows can only be present if the last round or this round's
-  // injection wrote some
-  const int mode = a.unfiltered ? SCAN_UNFILTERED : (c->lists_live ? SCAN_LISTS : SCAN_FILTERED);
+                       c->d_abits, c->d_ws, c->d_slot[c->cur], c->cur, c->n_alloc);
+  const int mode = a.unfiltered ? SCAN_UNFILTERED : SCAN_FILTERED;
   (void)hipEventRecord(c->ev[4], c->stream);
-  // (the flat kernel writes bitmap rows only: not while id-list rows are configured)
-  const bool flat = W <= 32 && W <= c->cfg.flat_max_words && c->list_max() == 0;
+  const bool flat = W <= 32 && W <= c->cfg.flat_max_words;
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
     const dim3 grid(grid_for(a.nloc, per_block));
     if constexpr (W <= 32) {
@@ -1602,8 +1438,6 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     const dim3 grid(grid_for(a.nloc, per_block));
     if (mode == SCAN_UNFILTERED)
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
-    else if (mode == SCAN_LISTS)
-      hipLaunchKernelGGL((k_expand<W, SCAN_LISTS>), grid, dim3(BLOCK), 0, c->stream, a);
     else
       hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
   }
@@ -1614,8 +1448,6 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     const dim3 grid(grid_for(h.n_items, WAVES));
     if (mode == SCAN_UNFILTERED)
       hipLaunchKernelGGL((k_hub_partial<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, h);
-    else if (mode == SCAN_LISTS)
-      hipLaunchKernelGGL((k_hub_partial<W, SCAN_LISTS>), grid, dim3(BLOCK), 0, c->stream, h);
     else
       hipLaunchKernelGGL((k_hub_partial<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, h);
     h.n_items = c->n_hubs;
@@ -1625,8 +1457,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 
 static int launch_expand(Ctx* c) {
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
-                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->list_max(), c->d_abits, c->d_sbits,
-                     c->n_alloc);
+                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc);
   // direction: push when the senders' arcs are a small share of all arcs
   const int r = c->round;
   // early exit pays once frontier rows are dense: >= m/16 new bits per vertex last round
@@ -1637,11 +1468,11 @@ static int launch_expand(Ctx* c) {
   if (c->mode_push && c->nloc() > 0)
     GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1] + c->vbegin, 0, (size_t)c->nloc() * 4, c->stream));
   // unfiltered pull when (nearly) every vertex is a sender: last round's
-  // receivers + this round's injected origins >= unfiltered_pct % of n
+  // receivers + this round's injected origins >= unfiltered_pct % of n.  Not
+  // with liveness: a crashed vertex's Message-List may hold bits it never sent.
   const double senders = (double)c->prev_receivers + (double)c->inj_groups_at(r);
-  c->unfiltered_now = !c->mode_push && c->cfg.unfiltered_pct > 0 &&
+  c->unfiltered_now = !c->mode_push && c->cfg.unfiltered_pct > 0 && !c->liveness_active &&
                       senders * 100.0 >= (double)c->cfg.unfiltered_pct * (double)c->n;
-  c->lists_live = c->list_max() > 0 && (c->prev_sp_written > 0 || c->inj_groups_at(r) > 0);
   ExpandArgs a{};
   fill_expand(c, a);
   a.unfiltered = c->unfiltered_now ? 1 : 0;
@@ -1730,12 +1561,14 @@ static int set_partition(Ctx* c, int32_t rank, int32_t nranks) {
 
 static void free_state(Ctx* c) {
   for (int k = 0; k < 2; ++k) {
-    dfree(&c->d_front[k]);
+    dfree(&c->d_slot[k]);
+    dfree(&c->d_frx[k]);
     dfree(&c->d_fpop[k]);
   }
-  dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
+  dfree(&c->d_sp); dfree(&c->d_ws);
+  dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_done_at);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
@@ -1774,10 +1607,15 @@ static int alloc_state(Ctx* c) {
   if (c->words <= 0) return set_error(GP_ESTATE, "no messages set");
   const size_t W = (size_t)c->words, na = (size_t)c->n_alloc, nl = (size_t)std::max<int64_t>(c->nloc(), 1);
   for (int k = 0; k < 2; ++k) {
-    GP_TRY(dalloc(&c->d_front[k], na * W));
+    GP_TRY(dalloc(&c->d_slot[k], na * W));
     GP_TRY(dalloc(&c->d_fpop[k], na));
+    // exact frontier rows only for per-message forwards (the pull reads whole
+    // Message-Lists)
+    if (c->cfg.track_msg_forwards) GP_TRY(dalloc(&c->d_frx[k], na * W));
+    else dfree(&c->d_frx[k]);
   }
-  GP_TRY(dalloc(&c->d_seen, nl * W));
+  GP_TRY(dalloc(&c->d_sp, na));
+  GP_TRY(dalloc(&c->d_ws, na));
   GP_TRY(dalloc(&c->d_seenpop, nl));
   if (c->cfg.track_first) GP_TRY(dalloc(&c->d_first, nl * W * 64));
   else dfree(&c->d_first);
@@ -1787,7 +1625,6 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_deg_live, na));
   GP_TRY(dalloc(&c->d_cand, na));
   GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
-  GP_TRY(dalloc(&c->d_sbits, (na + 63) / 64));
   GP_TRY(dalloc(&c->d_done_at, na));
   c->done_at_valid = false;
   GP_TRY(dalloc(&c->d_acc, na * W));
@@ -1806,7 +1643,7 @@ static int alloc_state(Ctx* c) {
   return 0;
 }
 
-static bool state_ready(const Ctx* c) { return c->d_seen != nullptr && c->d_front[0] != nullptr; }
+static bool state_ready(const Ctx* c) { return c->d_sp != nullptr && c->d_slot[0] != nullptr; }
 
 __global__ void k_midx(const int32_t* __restrict__ comp, const int32_t* __restrict__ idx_of_root,
                        int32_t* __restrict__ midx, int64_t n) {
@@ -1899,7 +1736,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->push_ratio = 40.0;   // push when sender arcs <= nnz / 40
   cfg->early_exit = 1;
   cfg->reserved0 = 0;
-  cfg->sparse_rows = 0;
+  cfg->reserved1 = 0;
   cfg->unfiltered_pct = 90;
   cfg->msg_word_base = 0;
   cfg->flat_max_words = 16;
@@ -1939,12 +1776,13 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_done_at);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
-  for (int k = 0; k < 2; ++k) { dfree(&c->d_front[k]); dfree(&c->d_fpop[k]); }
-  dfree(&c->d_seen); dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
+  for (int k = 0; k < 2; ++k) { dfree(&c->d_slot[k]); dfree(&c->d_frx[k]); dfree(&c->d_fpop[k]); }
+  dfree(&c->d_sp); dfree(&c->d_ws);
+  dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_stats);
   dfree(&c->d_hub_items); dfree(&c->d_hubs); dfree(&c->d_hub_item_ptr);
@@ -1962,6 +1800,7 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->hub_threshold < 64) return set_error(GP_EINVAL, "hub_threshold must be >= 64");
   if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
   if (cfg->msg_word_base < 0) return set_error(GP_EINVAL, "msg_word_base < 0");
+  if (cfg->reserved0 || cfg->reserved1) return set_error(GP_EINVAL, "reserved config fields must be 0");
   GP_HIP(hipSetDevice(c->device));
   const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
   c->cfg = *cfg;
@@ -2138,6 +1977,9 @@ int gp_reset(gp_ctx* c) {
   }
   const size_t W = (size_t)c->words, na = (size_t)c->n_alloc, nl = (size_t)std::max<int64_t>(c->nloc(), 1);
   hipStream_t s = c->stream;
+  // the slot buffers are not cleared: sp = none marks every row as absent
+  GP_HIP(hipMemsetAsync(c->d_sp, SLOT_NONE, na, s));
+  GP_HIP(hipMemsetAsync(c->d_ws, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_seenpop, 0, nl * 4, s));
   GP_HIP(hipMemsetAsync(c->d_fpop[0], 0, na * 4, s));
   GP_HIP(hipMemsetAsync(c->d_fpop[1], 0, na * 4, s));
@@ -2148,7 +1990,6 @@ int gp_reset(gp_ctx* c) {
   c->prev_next_arcs = 0;
   c->prev_new_bits = 0;
   c->prev_receivers = 0;
-  c->prev_sp_written = 0;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
   GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToDevice, s));
@@ -2235,10 +2076,13 @@ static int round_launch(Ctx* c) {
     ia.origin = c->d_inj_origin;
     ia.bits = c->d_inj_bits;
     ia.cnt = c->d_inj_cnt;
-    ia.front = c->d_front[c->cur];
+    ia.slot[0] = c->d_slot[0];
+    ia.slot[1] = c->d_slot[1];
+    ia.rslot = c->cur;
+    ia.sp = c->d_sp;
+    ia.ws = c->d_ws;
     ia.fpop = c->d_fpop[c->cur];
-    ia.list_max = c->list_max();
-    ia.seen = c->d_seen;
+    ia.frx = c->d_frx[0] ? c->d_frx[c->cur] : nullptr;
     ia.seenpop = c->d_seenpop;
     ia.first = c->cfg.track_first ? c->d_first : nullptr;
     ia.digest = c->cfg.track_digest ? c->d_digest : nullptr;
@@ -2257,9 +2101,8 @@ static int round_launch(Ctx* c) {
 
   if (c->cfg.track_msg_forwards) {   // sends of round r per message (owned senders)
     BitsumArgs b{};
-    b.rows = c->d_front[c->cur] + (size_t)c->vbegin * c->words;
+    b.rows = c->d_frx[c->cur] + (size_t)c->vbegin * c->words;   // exact frontier rows
     b.guard = c->d_fpop[c->cur] + c->vbegin;
-    b.list_max = c->list_max();
     b.weight = c->d_deg_live + c->vbegin;
     b.cnt = nullptr;
     b.wsum = c->d_msg_fwd;
@@ -2276,17 +2119,21 @@ static int round_launch(Ctx* c) {
   return 0;
 }
 
-// X_r over RCCL: all-gather the owned next rows + popcounts, sum the counters
+// X_r over RCCL: all-gather the owned rows of the slot written this round,
+// the popcounts and slot bytes (+ exact frontier rows when kept), sum the
+// counters.  Every rank then holds identical replicas for round r + 1.
 static int round_exchange_rccl(Ctx* c) {
   if (!c->comm) return 0;
   hipStream_t s = c->stream;
   const int nx = c->cur ^ 1;
-  const size_t W = (size_t)c->words;
+  const size_t W = (size_t)c->words, S = (size_t)c->slice, R = (size_t)c->rank;
   GP_RCCL(ncclGroupStart());
-  GP_RCCL(ncclAllGather(c->d_front[nx] + (size_t)c->rank * c->slice * W, c->d_front[nx],
-                        (size_t)c->slice * W, ncclUint64, c->comm, s));
-  GP_RCCL(ncclAllGather(c->d_fpop[nx] + (size_t)c->rank * c->slice, c->d_fpop[nx],
-                        (size_t)c->slice, ncclUint32, c->comm, s));
+  GP_RCCL(ncclAllGather(c->d_slot[nx] + R * S * W, c->d_slot[nx], S * W, ncclUint64, c->comm, s));
+  if (c->d_frx[0])
+    GP_RCCL(ncclAllGather(c->d_frx[nx] + R * S * W, c->d_frx[nx], S * W, ncclUint64, c->comm, s));
+  GP_RCCL(ncclAllGather(c->d_fpop[nx] + R * S, c->d_fpop[nx], S, ncclUint32, c->comm, s));
+  GP_RCCL(ncclAllGather(c->d_sp + R * S, c->d_sp, S, ncclUint8, c->comm, s));
+  GP_RCCL(ncclAllGather(c->d_ws + R * S, c->d_ws, S, ncclUint8, c->comm, s));
   // the report cursor (slot S_REPORT_CURSOR) stays rank-local
   GP_RCCL(ncclAllReduce(c->d_stats, c->d_stats, S_REPORT_CURSOR, ncclUint64, ncclSum, c->comm, s));
   GP_RCCL(ncclGroupEnd());
@@ -2319,8 +2166,6 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->rows_written = h[S_WRITTEN];
     out->vertices_visited = h[S_VISITED];
     out->atomics = h[S_ATOMICS];
-    out->sparse_gathered = h[S_SP_GATHERED];
-    out->sparse_written = h[S_SP_WRITTEN];
     out->next_arcs = h[S_NEXT_ARCS];
     out->mode = c->mode_push ? 1 : 0;
     out->unfiltered = (!c->mode_push && c->unfiltered_now) ? 1 : 0;
@@ -2343,7 +2188,6 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   c->prev_next_arcs = h[S_NEXT_ARCS];
   c->prev_new_bits = h[S_NEW_BITS];
   c->prev_receivers = h[S_RECEIVERS];
-  c->prev_sp_written = h[S_SP_WRITTEN];
   c->cur ^= 1;
   c->round = r + 1;
   return 0;
@@ -2386,10 +2230,16 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
       Ctx* src = ctxs[k];
       const int64_t b = src->vbegin, e = src->vend;
       if (e <= b) continue;
-      GP_HIP(hipMemcpyAsync(dst->d_front[nx] + (size_t)b * W, src->d_front[src->cur ^ 1] + (size_t)b * W,
+      const int sx = src->cur ^ 1;
+      GP_HIP(hipMemcpyAsync(dst->d_slot[nx] + (size_t)b * W, src->d_slot[sx] + (size_t)b * W,
                             (size_t)(e - b) * W * 8, hipMemcpyDefault, dst->stream));
-      GP_HIP(hipMemcpyAsync(dst->d_fpop[nx] + b, src->d_fpop[src->cur ^ 1] + b, (size_t)(e - b) * 4,
+      if (dst->d_frx[0] && src->d_frx[0])
+        GP_HIP(hipMemcpyAsync(dst->d_frx[nx] + (size_t)b * W, src->d_frx[sx] + (size_t)b * W,
+                              (size_t)(e - b) * W * 8, hipMemcpyDefault, dst->stream));
+      GP_HIP(hipMemcpyAsync(dst->d_fpop[nx] + b, src->d_fpop[sx] + b, (size_t)(e - b) * 4,
                             hipMemcpyDefault, dst->stream));
+      GP_HIP(hipMemcpyAsync(dst->d_sp + b, src->d_sp + b, (size_t)(e - b), hipMemcpyDefault, dst->stream));
+      GP_HIP(hipMemcpyAsync(dst->d_ws + b, src->d_ws + b, (size_t)(e - b), hipMemcpyDefault, dst->stream));
     }
   }
   gp_round_stats sum;
@@ -2406,7 +2256,6 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     sum.rows_gathered += st.rows_gathered; sum.seen_rows_read += st.seen_rows_read;
     sum.rows_written += st.rows_written; sum.vertices_visited += st.vertices_visited;
     sum.atomics += st.atomics; sum.next_arcs += st.next_arcs; sum.mode = st.mode;
-    sum.sparse_gathered += st.sparse_gathered; sum.sparse_written += st.sparse_written;
     sum.expand_ms = std::max(sum.expand_ms, st.expand_ms);
     sum.exchange_ms = std::max(sum.exchange_ms, st.exchange_ms);
     sum.round_ms = std::max(sum.round_ms, st.round_ms);
@@ -2414,6 +2263,7 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
   for (int32_t k = 0; k < nctx; ++k) {   // every context takes the same decisions next round
     ctxs[k]->prev_next_arcs = sum.next_arcs;
     ctxs[k]->prev_new_bits = sum.new_bits;
+    ctxs[k]->prev_receivers = sum.receivers;
   }
   if (out) *out = sum;
   return 0;
@@ -2447,9 +2297,9 @@ int gp_finalize_messages(gp_ctx* c) {
   GP_HIP(hipMemsetAsync(cov, 0, M * 8, s));
   if (fwd_from_seen) GP_HIP(hipMemsetAsync(fwd_local, 0, M * 8, s));
   BitsumArgs b{};
-  b.rows = c->d_seen;
-  b.guard = c->d_seenpop;   // rows with |seen| == 0 are stale (reset does not clear them)
-  b.list_max = 0;
+  b.slot[0] = c->d_slot[0] + (size_t)c->vbegin * c->words;   // seen row i = slot[sp[i]][i]
+  b.slot[1] = c->d_slot[1] + (size_t)c->vbegin * c->words;
+  b.sel = c->d_sp + c->vbegin;
   b.weight = c->d_deg_out + c->vbegin;
   b.cnt = cov;
   b.wsum = fwd_from_seen ? fwd_local : nullptr;
@@ -2482,13 +2332,18 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
     case GP_SEEN:
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(nl * W * 8));
-      if (bytes) {
-        GP_HIP(hipMemcpy(host, c->d_seen, (size_t)bytes, hipMemcpyDeviceToHost));
-        std::vector<uint32_t> sp((size_t)nl);
-        GP_HIP(hipMemcpy(sp.data(), c->d_seenpop, (size_t)nl * 4, hipMemcpyDeviceToHost));
+      if (bytes) {   // owned rows of both slots, picked per vertex by its slot byte
+        std::vector<uint64_t> s1((size_t)(nl * W));
+        std::vector<uint8_t> sp((size_t)nl);
+        const size_t off = (size_t)c->vbegin * W;
+        GP_HIP(hipMemcpy(host, c->d_slot[0] + off, (size_t)bytes, hipMemcpyDeviceToHost));
+        GP_HIP(hipMemcpy(s1.data(), c->d_slot[1] + off, (size_t)bytes, hipMemcpyDeviceToHost));
+        GP_HIP(hipMemcpy(sp.data(), c->d_sp + c->vbegin, (size_t)nl, hipMemcpyDeviceToHost));
         uint64_t* h = static_cast<uint64_t*>(host);
-        for (int64_t v = 0; v < nl; ++v)   // rows never written this run are stale
-          if (!sp[(size_t)v]) std::memset(h + v * W, 0, (size_t)W * 8);
+        for (int64_t v = 0; v < nl; ++v) {
+          if (sp[(size_t)v] == SLOT_NONE) std::memset(h + v * W, 0, (size_t)W * 8);
+          else if (sp[(size_t)v] == 1) std::memcpy(h + v * W, s1.data() + v * W, (size_t)W * 8);
+        }
       }
       return 0;
     case GP_FIRST:
@@ -2544,23 +2399,16 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       return 0;
     case GP_FRONTIER: {
       if (!run) return set_error(GP_ESTATE, "no run state");
+      // exact frontier rows exist only with track_msg_forwards: the pull reads
+      // whole Message-Lists
+      if (!c->d_frx[0]) return set_error(GP_ENOTRACK, "frontier rows are kept only with track_msg_forwards");
       GP_TRY(need(n * W * 8));
       std::vector<uint32_t> fp((size_t)n);
       GP_HIP(hipMemcpy(fp.data(), c->d_fpop[c->cur], (size_t)n * 4, hipMemcpyDeviceToHost));
-      GP_HIP(hipMemcpy(host, c->d_front[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
+      GP_HIP(hipMemcpy(host, c->d_frx[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
       uint64_t* h = static_cast<uint64_t*>(host);
-      const uint32_t lmax = (uint32_t)c->list_max();
-      for (int64_t v = 0; v < n; ++v) {
-        if (!fp[v]) {
-          std::memset(h + v * W, 0, (size_t)W * 8);
-        } else if (fp[v] <= lmax) {   // id-list row
-          uint16_t ids[LIST_SLOTS];
-          std::memcpy(ids, h + v * W, sizeof(ids));
-          std::memset(h + v * W, 0, (size_t)W * 8);
-          for (int q = 0; q < LIST_SLOTS; ++q)
-            if (ids[q] != SP_EMPTY) h[v * W + (ids[q] >> 6)] |= 1ull << (ids[q] & 63);
-        }
-      }
+      for (int64_t v = 0; v < n; ++v)
+        if (!fp[v]) std::memset(h + v * W, 0, (size_t)W * 8);
       return 0;
     }
     default:

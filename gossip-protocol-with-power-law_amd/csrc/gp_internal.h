@@ -22,13 +22,9 @@ typedef unsigned long long u64;
 enum StatSlot {
   S_INJECTED = 0, S_LOST, S_NEW_BITS, S_RECEIVERS, S_SENDS, S_ACTIVE, S_CRASHED,
   S_REPORTS, S_REMOVALS, S_DUP, S_ARCS, S_GATHERED, S_SEEN_READ, S_WRITTEN,
-  S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_SP_GATHERED, S_SP_WRITTEN, NST,
+  S_VISITED, S_NEXT_ARCS, S_ATOMICS, NST,
   S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR
 };
-
-// id-list frontier rows hold at most this many message ids (one 64-byte segment
-// of 32 u16 slots, 0xFFFF-padded)
-constexpr int LIST_MAX = 31;
 
 struct HubItem {       // one wave's share of a hub's in-list
   int32_t v;           // hub vertex
@@ -72,10 +68,14 @@ struct Ctx {
   uint32_t* d_inj_cnt = nullptr;
 
   // per-run state
-  u64* d_front[2] = {nullptr, nullptr};   // [n_alloc][W]
+  // Message-List slots: v's seen row lives in d_slot[d_sp[v]];
+  // round r reads S[r & 1] and writes S[(r + 1) & 1]; cur == r & 1
+  u64* d_slot[2] = {nullptr, nullptr};    // [n_alloc][W]
+  uint8_t* d_sp = nullptr;          // [n_alloc] slot of v's seen row (0xFF: none)
+  uint8_t* d_ws = nullptr;          // [n_alloc] bit p: slot p written this run
+  u64* d_frx[2] = {nullptr, nullptr};     // exact frontier rows (track_msg_forwards only)
   uint32_t* d_fpop[2] = {nullptr, nullptr};    // [n_alloc]
   int cur = 0;
-  u64* d_seen = nullptr;       // [nloc][W]
   uint32_t* d_seenpop = nullptr;    // [nloc]
   uint8_t* d_first = nullptr;       // [nloc][W*64]
   u64* d_digest = nullptr;     // [nloc]
@@ -83,10 +83,8 @@ struct Ctx {
   uint8_t* d_miss = nullptr;        // [n_alloc]
   int32_t* d_deg_live = nullptr;    // [n_alloc]
   int32_t* d_cand = nullptr;        // [n] detection candidates of a round
-  // [n_alloc/64] frontier_r bitmaps: active rows (fpop != 0) and id-list rows;
-  // separate arrays so the per-arc activity probe touches only 2 MB at 2^24
+  // [n_alloc/64] frontier_r activity bitmap (fpop != 0): 2 MB at 2^24
   u64* d_abits = nullptr;
-  u64* d_sbits = nullptr;
   // push (sparse-round) mode
   u64* d_acc = nullptr;             // [n_alloc][W] OR accumulator, kept all-zero between uses
   u64* d_tbits = nullptr;           // [n_alloc/64] receivers pushed to this round
@@ -100,8 +98,6 @@ struct Ctx {
   u64 prev_new_bits = 0;            // new bits of the last round (global)
   u64 prev_receivers = 0;           // receivers of the last round (global)
   bool unfiltered_now = false;      // this round's pull skips the activity check
-  u64 prev_sp_written = 0;          // id-list rows written by the last round (global)
-  bool lists_live = false;          // frontier_r may hold id-list rows
   int64_t inj_groups_at(int32_t r) const {
     auto it = inject.find(r);
     return it == inject.end() ? 0 : it->second.cnt;
@@ -141,8 +137,7 @@ struct Ctx {
   int cu_count = 256;
 
   int64_t nloc() const { return vend - vbegin; }
-  // frontier rows with at most this many bits are id lists
-  int32_t list_max() const { return (cfg.sparse_rows && words >= 16) ? LIST_MAX : 0; }
+
 };
 
 // error helpers (thread-local message, negative status)

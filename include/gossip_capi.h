@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 5
+#define GP_ABI_VERSION 6
 
 typedef struct gp_ctx gp_ctx;
 
@@ -65,14 +65,12 @@ typedef struct gp_round_stats {
   uint64_t removals;        /* vertices removed by the seed (Seed.py:387-391)        */
   uint64_t dup_reports;     /* reports hitting "not found" (Seed.py:373-375)         */
   uint64_t arcs_scanned;    /* in-arcs visited by the pull (byte accounting)         */
-  uint64_t rows_gathered;   /* neighbour frontier rows loaded (8*W bytes each)       */
+  uint64_t rows_gathered;   /* neighbour Message-List rows loaded (8*W bytes each)   */
   uint64_t seen_rows_read;  /* receiver seen rows read (8*W bytes each)              */
-  uint64_t rows_written;    /* next rows written (+ seen rows re-written)            */
+  uint64_t rows_written;    /* receiver seen rows written to the next slot (8*W B)   */
   uint64_t vertices_visited;/* receivers whose in-list was scanned                   */
   uint64_t atomics;         /* push mode: 64-bit atomicOr issued                      */
   uint64_t next_arcs;       /* out-degree sum of this round's receivers (direction)   */
-  uint64_t sparse_gathered; /* frontier rows read in id-list form (64 B each)        */
-  uint64_t sparse_written;  /* next rows written in id-list form                     */
   int32_t mode;             /* 0 = pull expansion, 1 = push expansion                 */
   int32_t unfiltered;       /* 1: the pull read every in-neighbour row without the
                                per-arc activity-bitmap check (dense round, §3.4)     */
@@ -103,8 +101,8 @@ typedef struct gp_config {
                                   0 = always pull                      */
   int32_t early_exit;          /* coverage-checked pull scans in dense rounds (§3.4)   */
   int32_t reserved0;           /* must be 0 (was a cache-steering knob; measured no effect) */
-  int32_t sparse_rows;         /* W >= 16: frontier rows with <= 31 bits are stored as
-                                  64-byte id lists in their row slot   */
+  int32_t reserved1;           /* must be 0 (was an id-list frontier-row format; the pull
+                                  now reads Message-List slots)         */
   int32_t unfiltered_pct;      /* pull without the per-arc activity check when >= this %
                                   of vertices are senders (0 = never)   */
   int32_t msg_word_base;       /* message shards: this context's message k
@@ -126,7 +124,8 @@ typedef enum gp_what {
   GP_DEG_LIVE = 7,    /* i32 [n]  neighbours not removed                             */
   GP_ROW_PTR = 8,     /* i64 [n+1] in-CSR offsets (as loaded / built)                */
   GP_COL = 9,         /* i32 [nnz] in-CSR columns                                    */
-  GP_FRONTIER = 10,   /* u64 [n][W] current frontier (rows with FPOP==0 read as 0)   */
+  GP_FRONTIER = 10,   /* u64 [n][W] current frontier (rows with FPOP==0 read as 0);
+                         kept only with track_msg_forwards (else GP_ENOTRACK)      */
   GP_FPOP = 11        /* u32 [n] |frontier(v)|                                       */
 } gp_what;
 

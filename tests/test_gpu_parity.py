@@ -35,11 +35,11 @@ MODE_IDS = ["pull", "pull-unfiltered", "push", "adaptive"]
 
 
 def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096,
-             push_ratio=10.0, sparse_rows=1, unfiltered_pct=90, flat_max_words=16, **kw):
+             push_ratio=10.0, unfiltered_pct=90, flat_max_words=16, **kw):
     churn = kw.get("churn", False)
     cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(bool(churn or crashes)),
                churn=int(churn), p_fail=kw.get("p_fail", 0.0), churn_seed=kw.get("churn_seed", 0),
-               hub_threshold=hub_threshold, push_ratio=push_ratio, sparse_rows=sparse_rows,
+               hub_threshold=hub_threshold, push_ratio=push_ratio,
                unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
     eng = _engine(pkg, g, origin, inject, **cfg)
     by_round = {}
@@ -261,30 +261,47 @@ def test_full_size_invariants_c3(pkg):
     assert sum(x["new_bits"] + x["injected"] for x in s1) == int(cov.sum())
 
 
-@pytest.mark.parametrize("sparse_rows", [0, 1])
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
-def test_wide_rows_sparse_format(pkg, oracle, mode, sparse_rows):
-    """W = 64 (4096 messages) with id-list frontier rows on and off, injections
-    spread over rounds, churn: exercises id lists through pull, push, injection
-    into an id-list row and per-message forwards."""
+def test_wide_rows_churn(pkg, oracle, mode):
+    """W = 64 (4096 messages), injections spread over rounds, churn: exercises
+    the Message-List slots through pull, push, injection into a sender's row,
+    the exact frontier rows kept for per-message forwards, and hub splits."""
     push_ratio, unfiltered_pct, flat_max_words = mode
     rp, col = oracle.chung_lu(60_000, 10, 2.4, 21)
     g = pkg.CSR(60_000, rp, col, False)
     m = 4096
     origin = pkg.overlay.random_origins(g.n, m, seed=21)
     inject = (np.arange(m) % 6).astype(np.int32)
-    cfg_first = push_ratio != 10.0   # first matrix on two of the three modes (1 GB host copy otherwise)
+    cfg_first = push_ratio != 10.0   # first matrix on three of the four modes (1 GB host copy otherwise)
     churn = dict(churn=True, p_fail=0.01, churn_seed=5)
-    eng_cfg = dict(push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
-    r = _compare(pkg, oracle, g, origin, inject, first=cfg_first, hub_threshold=512,
-                 sparse_rows=sparse_rows, **eng_cfg, **churn)
-    if sparse_rows:
-        assert sum(s["sparse_written"] for s in r["stats"]) > 0
-        if unfiltered_pct != 1:   # unfiltered rounds read id-list rows expanded to bitmaps
-            assert sum(s["sparse_gathered"] for s in r["stats"]) > 0
-    else:
-        assert sum(s["sparse_written"] for s in r["stats"]) == 0
+    r = _compare(pkg, oracle, g, origin, inject, first=cfg_first, hub_threshold=512, push_ratio=push_ratio,
+                 unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, **churn)
+    assert not any(s["unfiltered"] for s in r["stats"])   # never with liveness
     r["eng"].close()
+
+
+@pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
+def test_wide_rows_no_churn(pkg, oracle, mode):
+    """W = 64 without liveness: unfiltered dense rounds read whole Message-List
+    rows of every in-neighbour (stale slots zeroed by k_fixup_rows); repeated
+    runs on one context reuse the unclear slot buffers."""
+    push_ratio, unfiltered_pct, flat_max_words = mode
+    rp, col = oracle.chung_lu(60_000, 10, 2.4, 22)
+    g = pkg.CSR(60_000, rp, col, False)
+    m = 4096
+    origin = pkg.overlay.random_origins(g.n, m, seed=22)
+    inject = (np.arange(m) % 4).astype(np.int32)
+    r = _compare(pkg, oracle, g, origin, inject, first=False, push_ratio=push_ratio,
+                 unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
+    if unfiltered_pct == 1:
+        assert any(s["unfiltered"] for s in r["stats"])
+    eng, ref = r["eng"], r["ref"]
+    for _ in range(2):   # stale rows of the previous run must not leak in
+        eng.reset()
+        stats = eng.run()
+        assert [s["new_bits"] for s in stats] == [s["new_bits"] for s in ref["stats"]]
+        assert np.array_equal(eng.digest(), ref["digest"])
+    eng.close()
 
 
 @pytest.mark.parametrize("shards", [2, 4])
