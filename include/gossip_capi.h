@@ -22,9 +22,12 @@
  *     are packed 64 per uint64 word, W = ceil(m/64) rounded up to a power of two
  *     (1..64 words per vertex row, i.e. m <= 4096 per context; larger message
  *     sets are run as independent batches by the host -- messages never interact).
- *   - Multi-GPU: one process per GPU; each context owns a contiguous vertex
- *     slice [vbegin, vend) of equal size and exchanges frontier rows by RCCL
- *     all-gather over xGMI after every round (gp_comm_init).
+ *   - Multi-GPU: one process per GPU.  Either message shards (each context
+ *     runs the whole overlay for a word-aligned block of messages,
+ *     gp_config.msg_word_base; no collective), or a vertex partition: each
+ *     context owns a contiguous slice [vbegin, vend) of equal size and
+ *     exchanges its new Message-List rows by RCCL all-gather over xGMI after
+ *     every round (gp_comm_init).
  */
 #ifndef GOSSIP_CAPI_H
 #define GOSSIP_CAPI_H

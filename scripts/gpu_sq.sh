@@ -9,7 +9,7 @@ for tree in . _old; do
   mkdir -p $out
   i=0
   for P in "$P1" "$P2"; do
-    (cd $tree && timeout -s KILL 180 rocprofv3 --pmc $P --output-format csv -d $out/p$i -o p$i -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --sparse-rows 0 > $out/p$i.json 2> $out/p$i.err) || exit 1
+    (cd $tree && timeout -s KILL 180 rocprofv3 --pmc $P --output-format csv -d $out/p$i -o p$i -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $out/p$i.json 2> $out/p$i.err) || exit 1
     i=$((i+1))
   done
   python3 scripts/pmc_table.py $out k_expand > $out/table.md

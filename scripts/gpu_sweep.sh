@@ -2,8 +2,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/sweep
-PARAM=${PARAM:---hot-degree}
-for val in ${LIST:-0 64}; do
+PARAM=${PARAM:---push-ratio}
+for val in ${LIST:-40 16}; do
   tag=$(echo "$PARAM$val" | tr -c 'a-zA-Z0-9.' '_')
   timeout -k 10 120 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline $PARAM $val --profile-steps $EXTRA > gpurun_out/sweep/$tag.json 2> gpurun_out/sweep/$tag.err || exit 1
   python - "$tag" "$PARAM" "$val" <<'PY'
