@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--early-exit", type=int, default=1)
     ap.add_argument("--unfiltered-pct", type=int, default=90,
                     help="pull without the per-arc activity check when >= this %% of vertices send (0 = never)")
+    ap.add_argument("--arc-mask-permille", type=int, default=0,
+                    help="filtered pull rounds with >= this many senders per 1000 vertices build "
+                         "the per-arc activity mask first (0 = always probe per arc)")
     ap.add_argument("--flat-max-words", type=int, default=16,
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,13 +61,20 @@ def parse():
 def round_bytes(st, words, nloc):
     """Algorithmic bytes of one expansion launch of the pull:
     per owned vertex 21 B of vertex state (fpop, deg_live, row_ptr pair, state,
-    seenpop, done_at, slot byte), per scanned arc the 4-B column id (+ 8 B for
-    the activity-bitmap probe in filtered rounds), per gathered neighbour row
-    8W B, per receiver seen row read 8W B and per receiver seen row written
-    to the next slot 8W B."""
+    seenpop, done_at, slot byte), per scanned arc the 4-B column id + the 8-B
+    activity-bitmap probe (scan 0), or 1 mask bit + the 4-B column id of the
+    active arcs only (scan 1, + 8 B of mask words per vertex), or the column id
+    alone (scan 2, unfiltered), per gathered neighbour row 8W B, per receiver
+    seen row read 8W B and per receiver seen row written to the next slot 8W B."""
     w8 = 8 * words
-    arc = 4 if st.get("unfiltered") else 12
-    return (21 * nloc + arc * st["arcs_scanned"] + w8 * st["rows_gathered"] + w8 * st["seen_rows_read"]
+    scan = st.get("scan", 0)
+    if scan == 2:
+        arcs = 4 * st["arcs_scanned"]
+    elif scan == 1:
+        arcs = st["arcs_scanned"] / 8 + 4 * st["rows_gathered"] + 8 * nloc
+    else:
+        arcs = 12 * st["arcs_scanned"]
+    return (21 * nloc + arcs + w8 * st["rows_gathered"] + w8 * st["seen_rows_read"]
             + w8 * st["rows_written"])
 
 
@@ -122,7 +132,8 @@ def main():
     eng = pkg.GossipEngine(device, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
                            push_ratio=args.push_ratio,
                            early_exit=args.early_exit,
-                           unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words)
+                           unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words,
+                           arc_mask_permille=args.arc_mask_permille)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()
@@ -178,7 +189,7 @@ def main():
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
                                                 "rows_written", "atomics",
-                                                "unfiltered", "expand_ms", "kernel_ms", "exchange_ms")}),
+                                                "scan", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

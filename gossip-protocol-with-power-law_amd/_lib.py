@@ -48,7 +48,7 @@ class RoundStats(ctypes.Structure):
         ("atomics", ctypes.c_uint64),
         ("next_arcs", ctypes.c_uint64),
         ("mode", ctypes.c_int32),
-        ("unfiltered", ctypes.c_int32),
+        ("scan", ctypes.c_int32),
         ("expand_ms", ctypes.c_double),
         ("exchange_ms", ctypes.c_double),
         ("round_ms", ctypes.c_double),
@@ -76,7 +76,7 @@ class Config(ctypes.Structure):
         ("report_capacity", ctypes.c_int64),
         ("push_ratio", ctypes.c_double),
         ("early_exit", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("arc_mask_permille", ctypes.c_int32),
         ("reserved1", ctypes.c_int32),
         ("unfiltered_pct", ctypes.c_int32),
         ("msg_word_base", ctypes.c_int32),
@@ -115,7 +115,7 @@ SIGNATURES = {
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
 }
 
-ABI_VERSION = 6   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 7   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

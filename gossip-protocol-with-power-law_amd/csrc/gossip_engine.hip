@@ -34,6 +34,12 @@ int set_error(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+int copy_sync(Ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  if (bytes == 0) return 0;
+  GP_HIP(hipMemcpyAsync(dst, src, bytes, kind, c->stream));
+  GP_HIP(hipStreamSynchronize(c->stream));
+  return 0;
+}
 
 typedef unsigned long long u64;
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
@@ -170,6 +176,7 @@ struct ExpandArgs {
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
   int32_t early_exit;                  // this round scans with the coverage check
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
+  const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
   const uint32_t* __restrict__ done_at;// |messages of v's component|: seenpop == done_at -> done
   uint32_t* __restrict__ fpop_next;
   u64* __restrict__ frx;               // exact frontier rows of round r (track_msg_forwards only)
@@ -222,6 +229,8 @@ constexpr uint8_t SLOT_NONE = 0xFF;
 struct WaveLds {
   u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
   int32_t idx[64];      // active neighbours of one pass
+  uint32_t tot[64];     // k_expand: new bits of the wave's vertex k (committed after the loop)
+  u64 dig[64];          // k_expand: digest terms of vertex k
 };
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -258,9 +267,33 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
   }
 }
 
-// scan modes of a pull round (compile-time): the per-arc activity probe, or no
-// probe at all (unfiltered dense rounds: the bitmap misses L2 under the row stream)
-enum ScanMode { SCAN_FILTERED = 0, SCAN_UNFILTERED = 2 };
+// scan modes of a pull round (compile-time): the per-arc activity probe, the
+// per-arc activity mask built by k_arcmask before the round, or no check at all
+// (unfiltered dense rounds)
+enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2 };
+
+// activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
+// arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
+__device__ __forceinline__ u64 mask_window(const u64* __restrict__ amask, int64_t j0, int n) {
+  const int64_t k = j0 >> 6;
+  const int sh = (int)(j0 & 63);
+  u64 win = amask[k] >> sh;
+  if (sh) win |= amask[k + 1] << (64 - sh);
+  if (n < 64) win &= (1ull << n) - 1ull;
+  return win;
+}
+
+// any active arc in [b, e) (e > b)?  In-lists spanning more than two mask
+// words are taken as active (the scan finds out).
+__device__ __forceinline__ bool mask_any(const u64* __restrict__ amask, int64_t b, int64_t e) {
+  const int64_t k0 = b >> 6, k1 = (e - 1) >> 6;
+  if (k1 - k0 > 1) return true;
+  const u64 lo = ~0ull << (b & 63);
+  const int hi = (int)((e - 1) & 63);
+  const u64 him = hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1ull);
+  if (k0 == k1) return (amask[k0] & lo & him) != 0ull;
+  return ((amask[k0] & lo) | (amask[k1] & him)) != 0ull;
+}
 
 // neighbour u if its row is read this round, else -1
 template <int MODE>
@@ -343,11 +376,21 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
                                             int g, int lw, u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
   for (int64_t j0 = b; j0 < e; j0 += 64) {
     const int n = (int)min((int64_t)64, e - j0);
-    int32_t ent = -1;
-    if (lane < n) ent = probe<MODE>(a, a.gcol[j0 + lane]);
     st.add(S_ARCS, n);
-    const int cnt = stage_pass(L, ent);
-    if (cnt == 0) continue;
+    int cnt;
+    if constexpr (MODE == SCAN_MASKED) {
+      // the mask names the active arcs: column ids of the others are not loaded
+      const u64 win = mask_window(a.amask, j0, n);
+      if (win == 0ull) continue;
+      if ((win >> lane) & 1ull) L.idx[lane_rank(win)] = a.gcol[j0 + lane];
+      wave_sync_lds();
+      cnt = __popcll(win);
+    } else {
+      int32_t ent = -1;
+      if (lane < n) ent = probe<MODE>(a, a.gcol[j0 + lane]);
+      cnt = stage_pass(L, ent);
+      if (cnt == 0) continue;
+    }
     const bool stop = gather_rows<W>(a, L, cnt, g, lw, acc, st, ee, want);
     wave_sync_lds();
     if (stop) break;
@@ -376,14 +419,18 @@ __device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int w
 // receiver side of vertex v (local index i): new = acc & ~seen; write the new
 // seen row to slot wslot, counters.  have_sv: the seen row is parked in L.seen
 // (early exit), else it is loaded here from slot sv_slot.
-template <int W>
+// DEFER (k_expand): the per-vertex words (fpop, seenpop, slot bytes, digest)
+// go to L.tot/L.dig[k] and the wave commits them for its 64 vertices at once,
+// coalesced, after its loop -- one scattered read-modify-write chain less per
+// receiver, and whole cache lines instead of 1-8 byte pieces.
+template <int W, bool DEFER = false>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
                                            int g, int lw, WaveStats& st, WaveLds& L, bool have_sv,
-                                           uint32_t sv_slot) {
+                                           uint32_t sv_slot, int k = 0) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
-    if (lane == 0) a.fpop_next[v] = 0;
+    if (!DEFER && lane == 0) a.fpop_next[v] = 0;
     return;
   }
   if (!have_sv && sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
@@ -400,7 +447,7 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   const uint32_t pc = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
   const uint32_t tot = wave_sum_u32(pc);
   if (tot == 0) {
-    if (lane == 0) a.fpop_next[v] = 0;
+    if (!DEFER && lane == 0) a.fpop_next[v] = 0;
     return;
   }
   if (g == 0) {
@@ -419,18 +466,48 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
       if (WPL == 2 && nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + lw * WPL + 1), nw.y);
     }
     t = wave_xor_u64(t);
-    if (lane == 0) a.digest[i] ^= t;
+    if (DEFER) {
+      if (lane == 0) L.dig[k] = t;
+    } else if (lane == 0) {
+      a.digest[i] ^= t;
+    }
   }
-  if (lane == 0) {
-    a.fpop_next[v] = tot;
-    a.seenpop[i] += tot;
-    a.sp[v] = (uint8_t)a.wslot;
-    a.ws[v] |= (uint8_t)(1u << a.wslot);
+  if (DEFER) {
+    if (lane == 0) L.tot[k] = tot;
+  } else {
+    if (lane == 0) {
+      a.fpop_next[v] = tot;
+      a.seenpop[i] += tot;
+      a.sp[v] = (uint8_t)a.wslot;
+      a.ws[v] |= (uint8_t)(1u << a.wslot);
+    }
+    st.add(S_NEXT_ARCS, (u64)(uint32_t)max(a.deg_live[v], 0));
   }
   st.add(S_NEW_BITS, tot);
   st.add(S_RECEIVERS, 1);
   st.add(S_WRITTEN, 1);
-  st.add(S_NEXT_ARCS, (u64)(uint32_t)max(a.deg_live[v], 0));
+}
+
+// k_expand's commit of the deferred per-vertex words: lane k holds vertex
+// base + k (need: it was scanned)
+__device__ __forceinline__ void commit_vertices(const ExpandArgs& a, WaveLds& L, int64_t li, bool need,
+                                                WaveStats& st) {
+  wave_sync_lds();
+  const int lane = threadIdx.x & 63;
+  u64 next_arcs = 0;
+  if (need) {
+    const int v = (int)(a.vbegin + li);
+    const uint32_t tot = L.tot[lane];
+    a.fpop_next[v] = tot;
+    if (tot) {
+      a.seenpop[li] += tot;
+      a.sp[v] = (uint8_t)a.wslot;
+      a.ws[v] |= (uint8_t)(1u << a.wslot);
+      if (a.digest) a.digest[li] ^= L.dig[lane];
+      next_arcs = (u64)(uint32_t)max(a.deg_live[v], 0);
+    }
+  }
+  st.add(S_NEXT_ARCS, wave_sum_u64(next_arcs));
 }
 
 // main pull kernel: a wave owns 64 consecutive vertices.  The per-vertex
@@ -462,12 +539,15 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
       need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
+      if constexpr (MODE == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
       if (!need && !hub) a.fpop_next[v] = 0;
       slot_of = a.sp[v];
     }
     st.add(S_SENDS, wave_sum_u64(sends));
     st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
     st.add(S_VISITED, (u64)__popcll(__ballot(need)));
+    L.tot[lane] = 0u;
+    L.dig[lane] = 0ull;
     const bool ee = a.early_exit != 0;
     u64 m = __ballot(need);
     while (m) {
@@ -484,8 +564,9 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       }
       gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
-      finish_row<W>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot);
+      finish_row<W, true>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot, k);
     }
+    commit_vertices(a, L, li, need, st);
   }
   flush_stats(st, a.partial);
 }
@@ -992,6 +1073,37 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
   }
 }
 
+// per-arc activity mask of a filtered pull round: bit j of
+// amask[k] says whether sender gcol[64k + j] is active.  Probing here, with
+// no row stream evicting it, keeps the 2 MB activity bitmap L2-resident; the
+// pull then skips inactive arcs, and vertices without an active in-arc,
+// without loading their column ids.  AM_WORDS mask words per wave, over the
+// mask words [kbeg, kbeg + grid) covering the owned vertices' arcs.
+constexpr int AM_WORDS = 4;
+__global__ __launch_bounds__(BLOCK) void k_arcmask(const int32_t* __restrict__ gcol, const u64* __restrict__ abits,
+                                                   u64* __restrict__ amask, int64_t kbeg, int64_t nnz) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k0 = kbeg + ((int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6)) * AM_WORDS;
+  if (k0 * 64 >= nnz) return;
+  int32_t u[AM_WORDS];
+#pragma unroll
+  for (int q = 0; q < AM_WORDS; ++q) {
+    const int64_t e = (k0 + q) * 64 + lane;
+    u[q] = e < nnz ? gcol[e] : -1;
+  }
+  u64 w[AM_WORDS];
+#pragma unroll
+  for (int q = 0; q < AM_WORDS; ++q) w[q] = u[q] >= 0 ? abits[u[q] >> 6] : 0ull;
+  // one writer lane per word: selecting the four ballots into lanes 0-3 and
+  // storing from there (one dwordx2 store per wave) produced wrong words for
+  // the third ballot on gfx950, a few per 10^5 (found by scripts/debug_mask2.py)
+#pragma unroll
+  for (int q = 0; q < AM_WORDS; ++q) {
+    const u64 m = __ballot(u[q] >= 0 && ((w[q] >> (u[q] & 63)) & 1ull));
+    if (lane == 0 && (k0 + q) * 64 < nnz) amask[k0 + q] = m;
+  }
+}
+
 // unfiltered rounds: every in-neighbour row of S[r & 1] is
 // read, so each must be a subset of its vertex's Message-List -- true for
 // every row written this run (seen rows only grow).  Rows of inactive vertices
@@ -1365,6 +1477,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.ws = c->d_ws;
   a.fpop = c->d_fpop[c->cur];
   a.abits = c->d_abits;
+  a.amask = c->d_amask;
   a.frx = c->d_frx[0] ? c->d_frx[c->cur] : nullptr;
   a.frx_next = c->d_frx[0] ? c->d_frx[c->cur ^ 1] : nullptr;
   a.done_at = c->d_done_at;
@@ -1423,9 +1536,17 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   if (a.unfiltered)
     hipLaunchKernelGGL(k_fixup_rows<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
                        c->d_abits, c->d_ws, c->d_slot[c->cur], c->cur, c->n_alloc);
+  const bool flat = W <= 32 && W <= c->cfg.flat_max_words;
+  const bool masked = !a.unfiltered && !flat && c->arc_mask_now;
+  if (masked) {   // mask words of the owned vertices' in-arcs
+    const int64_t kb = c->h_row_ptr[(size_t)c->vbegin] >> 6;
+    const int64_t ke = (c->h_row_ptr[(size_t)c->vend] + 63) >> 6;
+    if (ke > kb)
+      hipLaunchKernelGGL(k_arcmask, dim3(grid_for(ke - kb, (int64_t)WAVES * AM_WORDS)), dim3(BLOCK), 0, c->stream,
+                         c->d_gcol, c->d_abits, c->d_amask, kb, c->nnz);
+  }
   const int mode = a.unfiltered ? SCAN_UNFILTERED : SCAN_FILTERED;
   (void)hipEventRecord(c->ev[4], c->stream);
-  const bool flat = W <= 32 && W <= c->cfg.flat_max_words;
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
     const dim3 grid(grid_for(a.nloc, per_block));
     if constexpr (W <= 32) {
@@ -1438,6 +1559,8 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     const dim3 grid(grid_for(a.nloc, per_block));
     if (mode == SCAN_UNFILTERED)
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+    else if (masked)
+      hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(BLOCK), 0, c->stream, a);
     else
       hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
   }
@@ -1473,6 +1596,10 @@ static int launch_expand(Ctx* c) {
   const double senders = (double)c->prev_receivers + (double)c->inj_groups_at(r);
   c->unfiltered_now = !c->mode_push && c->cfg.unfiltered_pct > 0 && !c->liveness_active &&
                       senders * 100.0 >= (double)c->cfg.unfiltered_pct * (double)c->n;
+  // filtered pull: probe every arc inside the scan, or build the per-arc mask
+  // first (pays once the probes are many: senders >= arc_mask_permille of n)
+  c->arc_mask_now = !c->mode_push && !c->unfiltered_now && c->cfg.arc_mask_permille > 0 &&
+                    senders * 1000.0 >= (double)c->cfg.arc_mask_permille * (double)c->n;
   ExpandArgs a{};
   fill_expand(c, a);
   a.unfiltered = c->unfiltered_now ? 1 : 0;
@@ -1539,11 +1666,11 @@ static int build_hubs(Ctx* c) {
   GP_TRY(dalloc(&c->d_hub_item_ptr, ptr.size()));
   GP_TRY(dalloc(&c->d_hub_pnz, c->h_hub_items.size()));
   if (!c->h_hub_items.empty())
-    GP_HIP(hipMemcpy(c->d_hub_items, c->h_hub_items.data(), c->h_hub_items.size() * sizeof(HubItem),
+    GP_TRY(copy_sync(c, c->d_hub_items, c->h_hub_items.data(), c->h_hub_items.size() * sizeof(HubItem),
                      hipMemcpyHostToDevice));
   if (!hubs.empty())
-    GP_HIP(hipMemcpy(c->d_hubs, hubs.data(), hubs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  GP_HIP(hipMemcpy(c->d_hub_item_ptr, ptr.data(), ptr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    GP_TRY(copy_sync(c, c->d_hubs, hubs.data(), hubs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, c->d_hub_item_ptr, ptr.data(), ptr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   if (c->words > 0) GP_TRY(dalloc(&c->d_hub_partial, c->h_hub_items.size() * (size_t)c->words));
   return 0;
 }
@@ -1568,7 +1695,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_sp); dfree(&c->d_ws);
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_done_at);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
@@ -1625,6 +1752,8 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_deg_live, na));
   GP_TRY(dalloc(&c->d_cand, na));
   GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
+  GP_TRY(dalloc(&c->d_amask, (size_t)((c->nnz + 63) / 64 + 2)));
+  GP_HIP(hipMemsetAsync(c->d_amask, 0, (size_t)((c->nnz + 63) / 64 + 2) * 8, c->stream));
   GP_TRY(dalloc(&c->d_done_at, na));
   c->done_at_valid = false;
   GP_TRY(dalloc(&c->d_acc, na * W));
@@ -1668,7 +1797,7 @@ static int compute_done_at(Ctx* c, int64_t groups) {
   dfree(&cnt);
   // component message masks (host: K <= #groups components carry messages)
   std::vector<int32_t> comp((size_t)c->n);
-  GP_HIP(hipMemcpy(comp.data(), c->d_comp, (size_t)c->n * 4, hipMemcpyDeviceToHost));
+  GP_TRY(copy_sync(c, comp.data(), c->d_comp, (size_t)c->n * 4, hipMemcpyDeviceToHost));
   std::vector<int32_t> idx_of_root((size_t)c->n, -1);
   std::vector<u64> masks;
   const size_t W = (size_t)c->words;
@@ -1684,10 +1813,10 @@ static int compute_done_at(Ctx* c, int64_t groups) {
   }
   if (masks.empty()) masks.assign(W, 0);
   GP_TRY(dalloc(&c->d_cmask, masks.size()));
-  GP_HIP(hipMemcpy(c->d_cmask, masks.data(), masks.size() * 8, hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, c->d_cmask, masks.data(), masks.size() * 8, hipMemcpyHostToDevice));
   int32_t* ior = nullptr;
   GP_TRY(dalloc(&ior, (size_t)c->n));
-  GP_HIP(hipMemcpy(ior, idx_of_root.data(), (size_t)c->n * 4, hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, ior, idx_of_root.data(), (size_t)c->n * 4, hipMemcpyHostToDevice));
   GP_TRY(dalloc(&c->d_midx, (size_t)c->n_alloc));
   // on the engine stream: the stream is non-blocking, so a null-stream memset
   // could land after k_midx
@@ -1735,7 +1864,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->report_capacity = 1 << 20;
   cfg->push_ratio = 40.0;   // push when sender arcs <= nnz / 40
   cfg->early_exit = 1;
-  cfg->reserved0 = 0;
+  cfg->arc_mask_permille = 0;   // per-arc mask off: its build costs what it saves
   cfg->reserved1 = 0;
   cfg->unfiltered_pct = 90;
   cfg->msg_word_base = 0;
@@ -1776,7 +1905,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_done_at);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -1800,7 +1929,8 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->hub_threshold < 64) return set_error(GP_EINVAL, "hub_threshold must be >= 64");
   if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
   if (cfg->msg_word_base < 0) return set_error(GP_EINVAL, "msg_word_base < 0");
-  if (cfg->reserved0 || cfg->reserved1) return set_error(GP_EINVAL, "reserved config fields must be 0");
+  if (cfg->reserved1) return set_error(GP_EINVAL, "reserved config fields must be 0");
+  if (cfg->arc_mask_permille < 0) return set_error(GP_EINVAL, "arc_mask_permille < 0");
   GP_HIP(hipSetDevice(c->device));
   const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
   c->cfg = *cfg;
@@ -1841,13 +1971,13 @@ int gp_load_graph(gp_ctx* c, int64_t n, int64_t nnz, const int64_t* row_ptr, con
   c->directed = directed ? 1 : 0;
   GP_TRY(dalloc(&c->d_row_ptr, (size_t)n + 1));
   GP_TRY(dalloc(&c->d_col, (size_t)nnz));
-  GP_HIP(hipMemcpy(c->d_row_ptr, row_ptr, ((size_t)n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-  if (nnz) GP_HIP(hipMemcpy(c->d_col, col, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, c->d_row_ptr, row_ptr, ((size_t)n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (nnz) GP_TRY(copy_sync(c, c->d_col, col, (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice));
   if (directed) {
     GP_TRY(dalloc(&c->d_out_row_ptr, (size_t)n + 1));
     GP_TRY(dalloc(&c->d_out_col, (size_t)nnz));
-    GP_HIP(hipMemcpy(c->d_out_row_ptr, orp.data(), ((size_t)n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-    if (nnz) GP_HIP(hipMemcpy(c->d_out_col, ocol.data(), (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    GP_TRY(copy_sync(c, c->d_out_row_ptr, orp.data(), ((size_t)n + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    if (nnz) GP_TRY(copy_sync(c, c->d_out_col, ocol.data(), (size_t)nnz * sizeof(int32_t), hipMemcpyHostToDevice));
   } else {
     dfree(&c->d_out_row_ptr);
     dfree(&c->d_out_col);
@@ -1956,9 +2086,9 @@ int gp_set_messages(gp_ctx* c, int32_t m, const int32_t* origin, const int32_t* 
   GP_TRY(dalloc(&c->d_inj_origin, g_origin.size()));
   GP_TRY(dalloc(&c->d_inj_bits, g_bits.size()));
   GP_TRY(dalloc(&c->d_inj_cnt, g_cnt.size()));
-  GP_HIP(hipMemcpy(c->d_inj_origin, g_origin.data(), g_origin.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  GP_HIP(hipMemcpy(c->d_inj_bits, g_bits.data(), g_bits.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-  GP_HIP(hipMemcpy(c->d_inj_cnt, g_cnt.data(), g_cnt.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, c->d_inj_origin, g_origin.data(), g_origin.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, c->d_inj_bits, g_bits.data(), g_bits.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, c->d_inj_cnt, g_cnt.data(), g_cnt.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   if (realloc || !state_ready(c)) GP_TRY(alloc_state(c));
   c->n_groups = (int64_t)g_origin.size();
   c->h_inj_origin = g_origin;
@@ -2011,12 +2141,12 @@ int gp_crash(gp_ctx* c, int32_t nverts, const int32_t* verts) {
   GP_HIP(hipSetDevice(c->device));
   std::vector<uint8_t> st((size_t)c->n);
   GP_HIP(hipStreamSynchronize(c->stream));
-  GP_HIP(hipMemcpy(st.data(), c->d_state, (size_t)c->n, hipMemcpyDeviceToHost));
+  GP_TRY(copy_sync(c, st.data(), c->d_state, (size_t)c->n, hipMemcpyDeviceToHost));
   for (int32_t k = 0; k < nverts; ++k) {
     if (verts[k] < 0 || verts[k] >= c->n) return set_error(GP_EINVAL, "vertex out of range");
     if (!(st[verts[k]] & ST_DOWN)) st[verts[k]] |= ST_PENDING;
   }
-  GP_HIP(hipMemcpy(c->d_state, st.data(), (size_t)c->n, hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, c->d_state, st.data(), (size_t)c->n, hipMemcpyHostToDevice));
   if (nverts > 0) {
     c->liveness_active = true;
     c->pending_crash = true;
@@ -2168,7 +2298,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->atomics = h[S_ATOMICS];
     out->next_arcs = h[S_NEXT_ARCS];
     out->mode = c->mode_push ? 1 : 0;
-    out->unfiltered = (!c->mode_push && c->unfiltered_now) ? 1 : 0;
+    out->scan = c->mode_push ? 0 : c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : 0;
     out->kernel_ms = 0.0;
     if (!c->mode_push && c->nloc() > 0) {
       float kms = 0.f;
@@ -2336,9 +2466,9 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
         std::vector<uint64_t> s1((size_t)(nl * W));
         std::vector<uint8_t> sp((size_t)nl);
         const size_t off = (size_t)c->vbegin * W;
-        GP_HIP(hipMemcpy(host, c->d_slot[0] + off, (size_t)bytes, hipMemcpyDeviceToHost));
-        GP_HIP(hipMemcpy(s1.data(), c->d_slot[1] + off, (size_t)bytes, hipMemcpyDeviceToHost));
-        GP_HIP(hipMemcpy(sp.data(), c->d_sp + c->vbegin, (size_t)nl, hipMemcpyDeviceToHost));
+        GP_TRY(copy_sync(c, host, c->d_slot[0] + off, (size_t)bytes, hipMemcpyDeviceToHost));
+        GP_TRY(copy_sync(c, s1.data(), c->d_slot[1] + off, (size_t)bytes, hipMemcpyDeviceToHost));
+        GP_TRY(copy_sync(c, sp.data(), c->d_sp + c->vbegin, (size_t)nl, hipMemcpyDeviceToHost));
         uint64_t* h = static_cast<uint64_t*>(host);
         for (int64_t v = 0; v < nl; ++v) {
           if (sp[(size_t)v] == SLOT_NONE) std::memset(h + v * W, 0, (size_t)W * 8);
@@ -2358,7 +2488,7 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       if (!run) return set_error(GP_ESTATE, "no run state");
       if (!c->cfg.track_digest) return set_error(GP_ENOTRACK, "track_digest is off");
       GP_TRY(need(nl * 8));
-      if (bytes) GP_HIP(hipMemcpy(host, c->d_digest, (size_t)bytes, hipMemcpyDeviceToHost));
+      if (bytes) GP_TRY(copy_sync(c, host, c->d_digest, (size_t)bytes, hipMemcpyDeviceToHost));
       return 0;
     case GP_COVERAGE:
     case GP_FORWARDS: {
@@ -2368,34 +2498,45 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       GP_TRY(need(M * 8));
       const size_t MM = (size_t)W * 64;
       const u64* src = c->d_msg_cov + (what == GP_COVERAGE ? 2 * MM : 3 * MM);
-      GP_HIP(hipMemcpy(host, src, (size_t)bytes, hipMemcpyDeviceToHost));
+      GP_TRY(copy_sync(c, host, src, (size_t)bytes, hipMemcpyDeviceToHost));
       return 0;
     }
     case GP_STATE:
     case GP_MISS:
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(n));
-      GP_HIP(hipMemcpy(host, what == GP_STATE ? c->d_state : c->d_miss, (size_t)n, hipMemcpyDeviceToHost));
+      GP_TRY(copy_sync(c, host, what == GP_STATE ? c->d_state : c->d_miss, (size_t)n, hipMemcpyDeviceToHost));
       return 0;
     case GP_DEG_LIVE:
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(n * 4));
-      GP_HIP(hipMemcpy(host, c->d_deg_live, (size_t)bytes, hipMemcpyDeviceToHost));
+      GP_TRY(copy_sync(c, host, c->d_deg_live, (size_t)bytes, hipMemcpyDeviceToHost));
       return 0;
     case GP_ROW_PTR:
       if (n <= 0) return set_error(GP_ESTATE, "no graph");
       GP_TRY(need((n + 1) * 8));
-      GP_HIP(hipMemcpy(host, c->d_row_ptr, (size_t)bytes, hipMemcpyDeviceToHost));
+      GP_TRY(copy_sync(c, host, c->d_row_ptr, (size_t)bytes, hipMemcpyDeviceToHost));
       return 0;
     case GP_COL:
       if (n <= 0) return set_error(GP_ESTATE, "no graph");
       GP_TRY(need(c->nnz * 4));
-      if (bytes) GP_HIP(hipMemcpy(host, c->d_col, (size_t)bytes, hipMemcpyDeviceToHost));
+      if (bytes) GP_TRY(copy_sync(c, host, c->d_col, (size_t)bytes, hipMemcpyDeviceToHost));
       return 0;
+#ifdef GP_DBG_READ   // scripts/debug_mask2.py: arc mask, gather-order columns, activity bits
+    case 100:
+      GP_TRY(copy_sync(c, host, c->d_amask, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case 101:
+      GP_TRY(copy_sync(c, host, c->d_gcol, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case 102:
+      GP_TRY(copy_sync(c, host, c->d_abits, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+#endif
     case GP_FPOP:
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(n * 4));
-      GP_HIP(hipMemcpy(host, c->d_fpop[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
+      GP_TRY(copy_sync(c, host, c->d_fpop[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
       return 0;
     case GP_FRONTIER: {
       if (!run) return set_error(GP_ESTATE, "no run state");
@@ -2404,8 +2545,8 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       if (!c->d_frx[0]) return set_error(GP_ENOTRACK, "frontier rows are kept only with track_msg_forwards");
       GP_TRY(need(n * W * 8));
       std::vector<uint32_t> fp((size_t)n);
-      GP_HIP(hipMemcpy(fp.data(), c->d_fpop[c->cur], (size_t)n * 4, hipMemcpyDeviceToHost));
-      GP_HIP(hipMemcpy(host, c->d_frx[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
+      GP_TRY(copy_sync(c, fp.data(), c->d_fpop[c->cur], (size_t)n * 4, hipMemcpyDeviceToHost));
+      GP_TRY(copy_sync(c, host, c->d_frx[c->cur], (size_t)bytes, hipMemcpyDeviceToHost));
       uint64_t* h = static_cast<uint64_t*>(host);
       for (int64_t v = 0; v < n; ++v)
         if (!fp[v]) std::memset(h + v * W, 0, (size_t)W * 8);
@@ -2422,7 +2563,7 @@ int gp_reports(gp_ctx* c, gp_report* buf, int64_t cap, int64_t* n_out) {
   const int64_t total = c->last_reports;
   *n_out = total;
   const int64_t k = std::min(std::min(total, cap), c->report_cap);
-  if (k > 0) GP_HIP(hipMemcpy(buf, c->d_reports, (size_t)k * sizeof(gp_report), hipMemcpyDeviceToHost));
+  if (k > 0) GP_TRY(copy_sync(c, buf, c->d_reports, (size_t)k * sizeof(gp_report), hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -85,6 +85,8 @@ struct Ctx {
   int32_t* d_cand = nullptr;        // [n] detection candidates of a round
   // [n_alloc/64] frontier_r activity bitmap (fpop != 0): 2 MB at 2^24
   u64* d_abits = nullptr;
+  // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
+  u64* d_amask = nullptr;
   // push (sparse-round) mode
   u64* d_acc = nullptr;             // [n_alloc][W] OR accumulator, kept all-zero between uses
   u64* d_tbits = nullptr;           // [n_alloc/64] receivers pushed to this round
@@ -98,6 +100,7 @@ struct Ctx {
   u64 prev_new_bits = 0;            // new bits of the last round (global)
   u64 prev_receivers = 0;           // receivers of the last round (global)
   bool unfiltered_now = false;      // this round's pull skips the activity check
+  bool arc_mask_now = false;        // this round's filtered pull reads the per-arc mask
   int64_t inj_groups_at(int32_t r) const {
     auto it = inject.find(r);
     return it == inject.end() ? 0 : it->second.cnt;
@@ -174,6 +177,11 @@ void dfree(T** p) {
   if (*p) { (void)hipFree(*p); *p = nullptr; }
 }
 
+// blocking copy ordered on the engine stream.  A plain hipMemcpy runs on the
+// null stream, which a non-blocking stream does not wait for (and a pageable
+// host-to-device hipMemcpy may return before its DMA lands), so kernels on
+// c->stream could read stale data or race with the copy.
+int copy_sync(Ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind);
 // graph_build.hip
 int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed);
 int build_gather_order(Ctx* c);

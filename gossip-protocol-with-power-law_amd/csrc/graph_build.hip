@@ -181,7 +181,7 @@ int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed) 
     A = (int64_t)nuniq;
     if (A > 0) {
       u64 last = 0;
-      GP_HIP(hipMemcpy(&last, ka + (A - 1), 8, hipMemcpyDeviceToHost));
+      GP_TRY(copy_sync(c, &last, ka + (A - 1), 8, hipMemcpyDeviceToHost));
       if (last == SENTINEL) --A;
     }
   }

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 6
+#define GP_ABI_VERSION 7
 
 typedef struct gp_ctx gp_ctx;
 
@@ -75,8 +75,9 @@ typedef struct gp_round_stats {
   uint64_t atomics;         /* push mode: 64-bit atomicOr issued                      */
   uint64_t next_arcs;       /* out-degree sum of this round's receivers (direction)   */
   int32_t mode;             /* 0 = pull expansion, 1 = push expansion                 */
-  int32_t unfiltered;       /* 1: the pull read every in-neighbour row without the
-                               per-arc activity-bitmap check (dense round, §3.4)     */
+  int32_t scan;             /* pull arc check: 0 = activity-bitmap probe per arc,
+                               1 = per-arc activity mask built first (§3.2),
+                               2 = none, every in-neighbour row read (§3.4)          */
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
@@ -103,7 +104,9 @@ typedef struct gp_config {
   double push_ratio;           /* push a round when its sender arcs * push_ratio <= nnz;
                                   0 = always pull                      */
   int32_t early_exit;          /* coverage-checked pull scans in dense rounds (§3.4)   */
-  int32_t reserved0;           /* must be 0 (was a cache-steering knob; measured no effect) */
+  int32_t arc_mask_permille;   /* filtered pull rounds with >= this many senders per 1000
+                                  vertices build the per-arc activity mask first
+                                  (0 = always probe per arc)           */
   int32_t reserved1;           /* must be 0 (was an id-list frontier-row format; the pull
                                   now reads Message-List slots)         */
   int32_t unfiltered_pct;      /* pull without the per-arc activity check when >= this %

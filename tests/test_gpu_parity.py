@@ -26,21 +26,23 @@ def _engine(pkg, g, origin, inject=None, **cfg):
     return eng
 
 
-# (push_ratio, unfiltered_pct, flat_max_words): always pull with the per-arc
-# activity filter, per-receiver kernel at every width; always pull, unfiltered
-# whenever >= 1 % of vertices send, edge-parallel kernel up to W = 32; always
-# push; adaptive direction + unfiltered dense rounds (the defaults)
-MODES = [(0.0, 0, 0), (0.0, 1, 32), (1e-12, 90, 16), (10.0, 90, 16)]
-MODE_IDS = ["pull", "pull-unfiltered", "push", "adaptive"]
+# (push_ratio, unfiltered_pct, flat_max_words, arc_mask_permille): always pull
+# with the per-arc activity probe, per-receiver kernel at every width; the same
+# with the per-arc activity mask whenever >= 0.1 % of vertices send; always
+# pull, unfiltered whenever >= 1 % of vertices send, edge-parallel kernel up to
+# W = 32; always push; adaptive direction + unfiltered dense rounds (defaults)
+MODES = [(0.0, 0, 0, 0), (0.0, 0, 0, 1), (0.0, 1, 32, 0), (1e-12, 90, 16, 10), (10.0, 90, 16, 10)]
+MODE_IDS = ["pull", "pull-masked", "pull-unfiltered", "push", "adaptive"]
 
 
 def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096,
-             push_ratio=10.0, unfiltered_pct=90, flat_max_words=16, **kw):
+             push_ratio=10.0, unfiltered_pct=90, flat_max_words=16, arc_mask_permille=10, **kw):
     churn = kw.get("churn", False)
     cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(bool(churn or crashes)),
                churn=int(churn), p_fail=kw.get("p_fail", 0.0), churn_seed=kw.get("churn_seed", 0),
                hub_threshold=hub_threshold, push_ratio=push_ratio,
-               unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
+               unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words,
+               arc_mask_permille=arc_mask_permille)
     eng = _engine(pkg, g, origin, inject, **cfg)
     by_round = {}
     for v, r in crashes:
@@ -78,15 +80,16 @@ def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_th
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_c2_ba_10k_64(pkg, oracle, mode):
     """BASELINE config 2: 10^4-node BA(m=2), 64 concurrent messages."""
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.barabasi_albert(10_000, 2, seed=2)
     origin = pkg.overlay.random_origins(g.n, 64, seed=2)
-    r = _compare(pkg, oracle, g, origin, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
+    r = _compare(pkg, oracle, g, origin, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
     if push_ratio == 1e-12:
         assert all(s["mode"] == 1 for s in r["stats"])
     if push_ratio == 0.0:
         assert all(s["mode"] == 0 for s in r["stats"])
-        assert any(s["unfiltered"] for s in r["stats"]) == (unfiltered_pct == 1)
+        assert any(s["scan"] == 2 for s in r["stats"]) == (unfiltered_pct == 1)
+        assert any(s["scan"] == 1 for s in r["stats"]) == (arc_mask == 1)
     total = sum(s["sends"] for s in r["stats"])
     assert total == 64 * g.nnz   # connected BA: every message crosses every arc once
     r["eng"].close()
@@ -95,23 +98,23 @@ def test_c2_ba_10k_64(pkg, oracle, mode):
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 @pytest.mark.parametrize("m", [1, 10, 63, 64, 65, 130, 300, 1000, 4096])
 def test_message_widths(pkg, oracle, m, mode):
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.barabasi_albert(1500, 3, seed=m)
     origin = pkg.overlay.random_origins(g.n, m, seed=m)
     inject = (np.arange(m) % 5).astype(np.int32)
-    _compare(pkg, oracle, g, origin, inject, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)["eng"].close()
+    _compare(pkg, oracle, g, origin, inject, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)["eng"].close()
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_hub_split(pkg, oracle, mode):
     """Force the multi-wave hub paths (pull: partials + final; push: grid-wide
     sweep of big senders) on every vertex above 64 arcs."""
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     rp, col = oracle.chung_lu(20_000, 8, 2.2, 11)
     g = pkg.CSR(20_000, rp, col, False)
     assert np.diff(rp).max() > 1000
     origin = pkg.overlay.random_origins(g.n, 256, seed=11)
-    _compare(pkg, oracle, g, origin, hub_threshold=64, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)["eng"].close()
+    _compare(pkg, oracle, g, origin, hub_threshold=64, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)["eng"].close()
 
 
 def test_c1_directed_schedule_and_direct_deliveries(pkg, oracle):
@@ -131,23 +134,23 @@ def test_c1_directed_schedule_and_direct_deliveries(pkg, oracle):
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_churn_random(pkg, oracle, mode):
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.barabasi_albert(5000, 2, seed=5)
     origin = pkg.overlay.random_origins(g.n, 128, seed=5)
     inject = (np.arange(128) % 9).astype(np.int32)
     r = _compare(pkg, oracle, g, origin, inject, churn=True, p_fail=0.03, churn_seed=77,
-                 push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
+                 push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
     assert sum(s["removals"] for s in r["stats"]) > 0
     r["eng"].close()
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_explicit_crashes_directed(pkg, oracle, mode):
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.first3_overlay(10)
     origin, inject, _ = pkg.peer.c1_schedule(10)
     r = _compare(pkg, oracle, g, np.array(origin, np.int32), np.array(inject, np.int32),
-                 crashes=[(4, 1), (0, 6), (9, 3)], push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
+                 crashes=[(4, 1), (0, 6), (9, 3)], push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
     assert sum(s["removals"] for s in r["stats"]) >= 2
     r["eng"].close()
 
@@ -165,9 +168,9 @@ def test_chung_lu_device_builder_matches_oracle(pkg, oracle):
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_c3_chung_lu_1e6_1024(pkg, oracle, mode):
     """BASELINE config 3: 10^6-node Chung-Lu (gamma 2.5), 1024 messages."""
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     n = 1_000_000
-    with pkg.GossipEngine(0, track_digest=1, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words) as eng:
+    with pkg.GossipEngine(0, track_digest=1, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask) as eng:
         eng.build_chung_lu(n, 8, 2.5, 3)
         g = eng.graph()
         origin = pkg.overlay.random_origins(n, 1024, seed=3)
@@ -189,7 +192,7 @@ def test_c3_chung_lu_1e6_1024(pkg, oracle, mode):
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_group_partition_invariance(pkg, oracle, mode):
     """2 and 3 contexts on one GPU (device-to-device exchange) == 1 context."""
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
     origin = pkg.overlay.random_origins(g.n, 200, seed=8)
     inject = (np.arange(200) % 4).astype(np.int32)
@@ -198,7 +201,7 @@ def test_group_partition_invariance(pkg, oracle, mode):
         engs = []
         for k in range(P):
             e = pkg.GossipEngine(0, track_first=1, churn=1, p_fail=0.02, churn_seed=3, track_msg_forwards=1,
-                                 push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
+                                 push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
             e.load_graph(g)
             e.set_partition(k, P)
             e.set_messages(origin, inject)
@@ -226,10 +229,10 @@ def test_group_partition_invariance(pkg, oracle, mode):
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_edge_cases(pkg, oracle, mode):
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     # isolated vertices, a single message, origin that crashes before injection
     g = pkg.CSR.from_edges(50, [(0, 1), (1, 2), (2, 3), (10, 11)])
-    kw = dict(push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
+    kw = dict(push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
     _compare(pkg, oracle, g, np.array([0], np.int32), **kw)["eng"].close()
     _compare(pkg, oracle, g, np.array([7, 7, 7], np.int32), **kw)["eng"].close()
     _compare(pkg, oracle, g, np.array([0, 10, 2], np.int32), np.array([0, 2, 4], np.int32),
@@ -266,7 +269,7 @@ def test_wide_rows_churn(pkg, oracle, mode):
     """W = 64 (4096 messages), injections spread over rounds, churn: exercises
     the Message-List slots through pull, push, injection into a sender's row,
     the exact frontier rows kept for per-message forwards, and hub splits."""
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     rp, col = oracle.chung_lu(60_000, 10, 2.4, 21)
     g = pkg.CSR(60_000, rp, col, False)
     m = 4096
@@ -275,8 +278,8 @@ def test_wide_rows_churn(pkg, oracle, mode):
     cfg_first = push_ratio != 10.0   # first matrix on three of the four modes (1 GB host copy otherwise)
     churn = dict(churn=True, p_fail=0.01, churn_seed=5)
     r = _compare(pkg, oracle, g, origin, inject, first=cfg_first, hub_threshold=512, push_ratio=push_ratio,
-                 unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, **churn)
-    assert not any(s["unfiltered"] for s in r["stats"])   # never with liveness
+                 unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask, **churn)
+    assert not any(s["scan"] == 2 for s in r["stats"])   # never unfiltered with liveness
     r["eng"].close()
 
 
@@ -285,16 +288,16 @@ def test_wide_rows_no_churn(pkg, oracle, mode):
     """W = 64 without liveness: unfiltered dense rounds read whole Message-List
     rows of every in-neighbour (stale slots zeroed by k_fixup_rows); repeated
     runs on one context reuse the unclear slot buffers."""
-    push_ratio, unfiltered_pct, flat_max_words = mode
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     rp, col = oracle.chung_lu(60_000, 10, 2.4, 22)
     g = pkg.CSR(60_000, rp, col, False)
     m = 4096
     origin = pkg.overlay.random_origins(g.n, m, seed=22)
     inject = (np.arange(m) % 4).astype(np.int32)
     r = _compare(pkg, oracle, g, origin, inject, first=False, push_ratio=push_ratio,
-                 unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words)
+                 unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
     if unfiltered_pct == 1:
-        assert any(s["unfiltered"] for s in r["stats"])
+        assert any(s["scan"] == 2 for s in r["stats"])
     eng, ref = r["eng"], r["ref"]
     for _ in range(2):   # stale rows of the previous run must not leak in
         eng.reset()
