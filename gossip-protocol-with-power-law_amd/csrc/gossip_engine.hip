@@ -231,6 +231,8 @@ struct WaveLds {
   int32_t idx[64];      // active neighbours of one pass
   uint32_t tot[64];     // k_expand: new bits of the wave's vertex k (committed after the loop)
   u64 dig[64];          // k_expand: digest terms of vertex k
+  int64_t rp[65];       // k_expand: row_ptr of the wave's vertices (rp[k], rp[k + 1])
+  int32_t mi[64];       // k_expand: component-mask row of vertex k (early-exit rounds)
 };
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -356,12 +358,12 @@ __device__ __forceinline__ u64x2 load_seen(const ExpandArgs& a, int v, uint32_t 
 // return, in group-0 lanes, the messages of its component it still lacks
 template <int W>
 __device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, WaveLds& L, int g, int lw,
-                                                   uint32_t sv_slot) {
+                                                   uint32_t sv_slot, int32_t mrow) {
   constexpr int WPL = Geo<W>::WPL;
   u64x2 want = {0, 0};
   if (g == 0) {
     const u64x2 sv = load_seen<W>(a, v, sv_slot, lw);
-    const u64x2 cm = load_piece<W>(a.cmask, a.midx[v], lw);
+    const u64x2 cm = load_piece<W>(a.cmask, mrow, lw);
     L.seen[lw * WPL] = sv.x;
     if constexpr (WPL == 2) L.seen[lw * WPL + 1] = sv.y;
     want = cm & ~sv;
@@ -537,17 +539,21 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       act = fp != 0u;
       if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
       const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
+      L.rp[lane] = b;
+      if (lane == 63 || li + 1 == a.nloc) L.rp[lane + 1] = e;
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
       need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
       if constexpr (MODE == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
       if (!need && !hub) a.fpop_next[v] = 0;
       slot_of = a.sp[v];
+      if (a.early_exit && need) L.mi[lane] = a.midx[v];
     }
     st.add(S_SENDS, wave_sum_u64(sends));
     st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
     st.add(S_VISITED, (u64)__popcll(__ballot(need)));
     L.tot[lane] = 0u;
     L.dig[lane] = 0ull;
+    wave_sync_lds();
     const bool ee = a.early_exit != 0;
     u64 m = __ballot(need);
     while (m) {
@@ -555,12 +561,12 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       m &= m - 1;
       const int64_t i = base + k;
       const int v = uniform((int)(a.vbegin + i));
-      const int64_t vb = a.row_ptr[v], ve = a.row_ptr[v + 1];   // scalar loads
+      const int64_t vb = L.rp[k], ve = L.rp[k + 1];   // staged by the lane phase
       const uint32_t sv_slot = (uint32_t)__builtin_amdgcn_readlane((int)slot_of, k);
       u64x2 acc = {0, 0}, want = {0, 0};
       if (ee) {
         if (sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
-        want = early_exit_target<W>(a, v, L, g, lw, sv_slot);
+        want = early_exit_target<W>(a, v, L, g, lw, sv_slot, L.mi[k]);
       }
       gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
@@ -814,7 +820,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
     if (!(a.state[h.v] & ST_DOWN) && a.seenpop[i] < a.done_at[h.v]) {
       const bool ee = a.early_exit != 0;
       u64x2 want = {0, 0};
-      if (ee) want = early_exit_target<W>(a, h.v, s_w[wib], g, lw, a.sp[h.v]);
+      if (ee) want = early_exit_target<W>(a, h.v, s_w[wib], g, lw, a.sp[h.v], a.midx[h.v]);
       gather_scan<W, MODE>(a, h.beg, h.end, s_w[wib], lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
     }
