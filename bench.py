@@ -64,8 +64,10 @@ def round_bytes(st, words, nloc):
     seenpop, done_at, slot byte), per scanned arc the 4-B column id + the 8-B
     activity-bitmap probe (scan 0), or 1 mask bit + the 4-B column id of the
     active arcs only (scan 1, + 8 B of mask words per vertex), or the column id
-    alone (scan 2, unfiltered), per gathered neighbour row 8W B, per receiver
-    seen row read 8W B and per receiver seen row written to the next slot 8W B."""
+    alone (scan 2, unfiltered), the neighbour-row bytes the kernel actually
+    loaded (8W per gathered row, less the words early-exit rounds skip), per
+    receiver seen row read 8W B and per receiver seen row written to the next
+    slot 8W B."""
     w8 = 8 * words
     scan = st.get("scan", 0)
     if scan == 2:
@@ -74,7 +76,7 @@ def round_bytes(st, words, nloc):
         arcs = st["arcs_scanned"] / 8 + 4 * st["rows_gathered"] + 8 * nloc
     else:
         arcs = 12 * st["arcs_scanned"]
-    return (21 * nloc + arcs + w8 * st["rows_gathered"] + w8 * st["seen_rows_read"]
+    return (21 * nloc + arcs + st["row_bytes"] + w8 * st["seen_rows_read"]
             + w8 * st["rows_written"])
 
 
@@ -188,7 +190,7 @@ def main():
         for s in runs[-1]:
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
-                                                "rows_written", "atomics",
+                                                "rows_written", "row_bytes", "atomics",
                                                 "scan", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None

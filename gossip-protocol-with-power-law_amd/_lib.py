@@ -47,6 +47,7 @@ class RoundStats(ctypes.Structure):
         ("vertices_visited", ctypes.c_uint64),
         ("atomics", ctypes.c_uint64),
         ("next_arcs", ctypes.c_uint64),
+        ("row_bytes", ctypes.c_uint64),
         ("mode", ctypes.c_int32),
         ("scan", ctypes.c_int32),
         ("expand_ms", ctypes.c_double),
@@ -115,7 +116,7 @@ SIGNATURES = {
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
 }
 
-ABI_VERSION = 7   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 8   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

@@ -310,30 +310,46 @@ __device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
 // OR the staged rows of one pass (L.idx[0, cnt)) into acc, GP_ROWS_IN_FLIGHT
 // wave-instructions of 16 B per lane in flight.  Early exit (bottom-up,
 // Beamer et al. SC'12): with `ee` the wave stops once acc | seen covers every
-// message of the vertex's component (want = cm & ~seen, group-0 lanes); OR is
-// idempotent, so acc & ~seen is exactly what the full scan would give.
-// Returns true on early exit.
+// message of the vertex's component (want = cm & ~seen); OR is idempotent, so
+// acc & ~seen is exactly what the full scan would give.  Per word, the same
+// rule skips the loads of a lane whose words are already complete (`miss`,
+// carried across passes): a 128-B line of a row is not fetched once its 16
+// words are.  Returns true on early exit.
+#ifndef GP_WORD_SKIP
+#define GP_WORD_SKIP 1
+#endif
 template <int W>
 __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, WaveLds& L, int cnt, int g, int lw, u64x2& acc,
                                             WaveStats& st, bool ee, u64x2 want) {
   constexpr int RPI = Geo<W>::RPI;
+  bool live = true;   // this lane's words still miss messages
+  if (GP_WORD_SKIP && ee) {
+    u64x2 t = acc;
+    reduce_slots<W>(t);
+    const u64x2 miss = want & ~t;
+    live = (miss.x | miss.y) != 0ull;
+  }
   for (int k0 = 0; k0 < cnt; k0 += GP_ROWS_IN_FLIGHT * RPI) {
     u64x2 r[GP_ROWS_IN_FLIGHT];
 #pragma unroll
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
       const int k = k0 + g + q * RPI;
       r[q] = u64x2{0, 0};
-      if (k < cnt) r[q] = load_piece<W>(a.rows, L.idx[k], lw);
+      if (k < cnt && live) r[q] = load_piece<W>(a.rows, L.idx[k], lw);
     }
 #pragma unroll
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
     st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
+    u64 pieces = 0;   // 8 * WPL-byte pieces actually loaded (word skip)
+#pragma unroll
+    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) pieces += (u64)__popcll(__ballot(k0 + g + q * RPI < cnt && live));
+    st.add(S_ROW_BYTES, pieces * (u64)(8 * Geo<W>::WPL));
     if (ee) {
       u64x2 t = acc;
       reduce_slots<W>(t);
-      u64x2 miss = {0, 0};
-      if (g == 0) miss = want & ~t;
-      if (!__any((miss.x | miss.y) != 0ull)) return true;
+      const u64x2 miss = want & ~t;
+      live = (miss.x | miss.y) != 0ull;
+      if (!__any(live)) return true;
     }
   }
   return false;
@@ -360,15 +376,15 @@ template <int W>
 __device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, WaveLds& L, int g, int lw,
                                                    uint32_t sv_slot, int32_t mrow) {
   constexpr int WPL = Geo<W>::WPL;
-  u64x2 want = {0, 0};
+  // every row slot group loads the same pieces (one fetch per line): each lane
+  // needs its words' target to skip the loads of words already complete
+  const u64x2 sv = load_seen<W>(a, v, sv_slot, lw);
+  const u64x2 cm = load_piece<W>(a.cmask, mrow, lw);
   if (g == 0) {
-    const u64x2 sv = load_seen<W>(a, v, sv_slot, lw);
-    const u64x2 cm = load_piece<W>(a.cmask, mrow, lw);
     L.seen[lw * WPL] = sv.x;
     if constexpr (WPL == 2) L.seen[lw * WPL + 1] = sv.y;
-    want = cm & ~sv;
   }
-  return want;
+  return cm & ~sv;
 }
 
 // per-receiver scan of arcs [b, e): 64 arcs per pass -- column ids, activity
@@ -745,6 +761,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       }
     }
     st.add(S_GATHERED, gathered);
+    st.add(S_ROW_BYTES, gathered * (u64)(8 * W));
     // receiver side, one receiver per lane: two passes over the row (count,
     // then write) so that a receiver with nothing new writes nothing
     u64 nbits = 0, nrecv = 0, nwritten = 0, narcs = 0, nseen = 0;
@@ -997,6 +1014,7 @@ __global__ __launch_bounds__(BLOCK) void k_push(ExpandArgs a) {
     const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
     const int64_t jb = a.orp[u], je = a.orp[u + 1];
     st.add(S_GATHERED, 1);
+    st.add(S_ROW_BYTES, (u64)(8 * W));
     st.add(S_ARCS, (u64)(je - jb));
     st.add(S_ATOMICS, (u64)(je - jb) * (u64)nnz);
     push_arcs<W>(a, jb, je, s_row[wib], s_words[wib], nnz, lane);
@@ -1027,6 +1045,7 @@ __global__ __launch_bounds__(BLOCK) void k_push_big(ExpandArgs a) {
     if (c0 == 0 && gw == (k * 7919) % nw) {
       push_sender_stats(a, u, st);
       st.add(S_GATHERED, 1);
+      st.add(S_ROW_BYTES, (u64)(8 * W));
     }
     if (c0 >= nch) continue;
     const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
@@ -2303,6 +2322,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->vertices_visited = h[S_VISITED];
     out->atomics = h[S_ATOMICS];
     out->next_arcs = h[S_NEXT_ARCS];
+    out->row_bytes = h[S_ROW_BYTES];
     out->mode = c->mode_push ? 1 : 0;
     out->scan = c->mode_push ? 0 : c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : 0;
     out->kernel_ms = 0.0;
@@ -2392,6 +2412,7 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     sum.rows_gathered += st.rows_gathered; sum.seen_rows_read += st.seen_rows_read;
     sum.rows_written += st.rows_written; sum.vertices_visited += st.vertices_visited;
     sum.atomics += st.atomics; sum.next_arcs += st.next_arcs; sum.mode = st.mode;
+    sum.row_bytes += st.row_bytes;
     sum.expand_ms = std::max(sum.expand_ms, st.expand_ms);
     sum.exchange_ms = std::max(sum.exchange_ms, st.exchange_ms);
     sum.round_ms = std::max(sum.round_ms, st.round_ms);

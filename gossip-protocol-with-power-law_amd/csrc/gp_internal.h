@@ -22,7 +22,7 @@ typedef unsigned long long u64;
 enum StatSlot {
   S_INJECTED = 0, S_LOST, S_NEW_BITS, S_RECEIVERS, S_SENDS, S_ACTIVE, S_CRASHED,
   S_REPORTS, S_REMOVALS, S_DUP, S_ARCS, S_GATHERED, S_SEEN_READ, S_WRITTEN,
-  S_VISITED, S_NEXT_ARCS, S_ATOMICS, NST,
+  S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_ROW_BYTES, NST,
   S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR
 };
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 7
+#define GP_ABI_VERSION 8
 
 typedef struct gp_ctx gp_ctx;
 
@@ -74,6 +74,8 @@ typedef struct gp_round_stats {
   uint64_t vertices_visited;/* receivers whose in-list was scanned                   */
   uint64_t atomics;         /* push mode: 64-bit atomicOr issued                      */
   uint64_t next_arcs;       /* out-degree sum of this round's receivers (direction)   */
+  uint64_t row_bytes;       /* bytes of neighbour rows actually loaded (the pull skips
+                               the words a receiver already completed, §3.4)         */
   int32_t mode;             /* 0 = pull expansion, 1 = push expansion                 */
   int32_t scan;             /* pull arc check: 0 = activity-bitmap probe per arc,
                                1 = per-arc activity mask built first (§3.2),

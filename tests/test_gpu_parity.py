@@ -66,6 +66,10 @@ def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_th
         for k in STAT_KEYS:
             assert a[k] == b[k], (k, a["round"], a[k], b[k])
     W = eng.words
+    for s in stats:   # word skip only ever drops loads
+        assert s["row_bytes"] <= 8 * W * s["rows_gathered"], s
+        if s["mode"] == 1:
+            assert s["row_bytes"] == 8 * W * s["rows_gathered"], s
     assert np.array_equal(eng.seen(), ref["seen"][:, :W])
     if first:
         assert np.array_equal(eng.first(), ref["first"])
