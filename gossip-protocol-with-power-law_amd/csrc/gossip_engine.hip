@@ -251,6 +251,27 @@ __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t x, int lane) {
   return inc - x;
 }
 
+// reductions over the LPR lanes of one row slot (lanes g*LPR .. g*LPR + LPR - 1)
+template <int LPR>
+__device__ __forceinline__ bool group_or(bool x) {
+  uint32_t y = x ? 1u : 0u;
+#pragma unroll
+  for (int s = 1; s < LPR; s <<= 1) y |= (uint32_t)__shfl_xor((int)y, s);
+  return y != 0u;
+}
+template <int LPR>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+#pragma unroll
+  for (int s = 1; s < LPR; s <<= 1) x += (uint32_t)__shfl_xor((int)x, s);
+  return x;
+}
+template <int LPR>
+__device__ __forceinline__ u64 group_xor(u64 x) {
+#pragma unroll
+  for (int s = 1; s < LPR; s <<= 1) x ^= __shfl_xor(x, s);
+  return x;
+}
+
 __device__ __forceinline__ u64 wave_sum_u64(u64 x) {
 #pragma unroll
   for (int s = 32; s > 0; s >>= 1) x += __shfl_xor(x, s);
@@ -614,6 +635,9 @@ struct FlatLds {
   int32_t idx[64];              // active neighbours of one chunk
   int8_t vtx[64];               // their receiver (lane) in the wave
   int8_t own[FLAT_CAP];         // receiver lane owning each arc position of the window
+  uint32_t tot[64];             // receiver side: new bits of receiver k
+  u64 dig[64];                  // its digest terms
+  int8_t rd[64];                // its seen row was read
 };
 
 template <int W, int MODE>
@@ -762,52 +786,63 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
     }
     st.add(S_GATHERED, gathered);
     st.add(S_ROW_BYTES, gathered * (u64)(8 * W));
-    // receiver side, one receiver per lane: two passes over the row (count,
-    // then write) so that a receiver with nothing new writes nothing
+    // receiver side: RPI receivers per wave-instruction, LPR lanes x 16 B per
+    // row (coalesced, like the gather); a receiver with nothing new reads and
+    // writes nothing.  Per-receiver words go to F.tot / F.dig, then one
+    // coalesced commit with one receiver per lane.
+    wave_sync_lds();
+    const u64 needm = __ballot(need);
+    for (int r0 = 0; r0 < 64; r0 += RPI) {
+      const int r = r0 + g;
+      const uint32_t rslot = (uint32_t)__shfl((int)slot_of, r);
+      const int rv = __shfl(v, r);
+      const bool rn = (needm >> r) & 1ull;
+      u64x2 accp = {0, 0};
+      if (rn) {
+        accp.x = F.acc[r][lw * WPL];
+        if constexpr (WPL == 2) accp.y = F.acc[r][lw * WPL + 1];
+      }
+      const bool any = group_or<LPR>((accp.x | accp.y) != 0ull);
+      u64x2 sv = {0, 0};
+      if (any && rslot != SLOT_NONE) sv = load_piece<W>(a.slot[rslot], rv, lw);
+      const u64x2 nw = accp & ~sv;
+      const uint32_t tot = group_sum<LPR>((uint32_t)(__popcll(nw.x) + __popcll(nw.y)));
+      u64 t = 0;
+      if (tot) {
+        store_piece<W>(a.slot[a.wslot], rv, lw, sv | nw);
+        if (a.frx_next) store_piece<W>(a.frx_next, rv, lw, nw);
+        if (a.first) {
+          uint8_t* row = a.first + (size_t)(base + r) * (W * 64);
+          if (nw.x) set_first_bytes(row, lw * WPL, nw.x, (uint32_t)a.rr);
+          if (WPL == 2 && nw.y) set_first_bytes(row, lw * WPL + 1, nw.y, (uint32_t)a.rr);
+        }
+        if (a.digest) {
+          if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + lw * WPL), nw.x);
+          if (WPL == 2 && nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + lw * WPL + 1), nw.y);
+        }
+      }
+      t = group_xor<LPR>(t);
+      if (lw == 0) {
+        F.tot[r] = tot;
+        F.dig[r] = t;
+        F.rd[r] = (int8_t)(any && rslot != SLOT_NONE);
+      }
+    }
+    wave_sync_lds();
     u64 nbits = 0, nrecv = 0, nwritten = 0, narcs = 0, nseen = 0;
     if (need) {
-      u64 any = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) any |= F.acc[lane][w];
-      if (!any) {
-        a.fpop_next[v] = 0;
-      } else {
-        const u64* __restrict__ srow = slot_of != SLOT_NONE ? a.slot[slot_of] + (size_t)v * W : nullptr;
-        if (srow) nseen = 1;
-        uint32_t tot = 0;
-#pragma unroll 4
-        for (int w = 0; w < W; ++w) {
-          const u64 s = srow ? srow[w] : 0ull;
-          const u64 nw = F.acc[lane][w] & ~s;
-          F.acc[lane][w] = nw;
-          tot += (uint32_t)__popcll(nw);
-        }
-        a.fpop_next[v] = tot;
-        if (tot) {
-          u64 dig = 0;
-          u64* __restrict__ drow = a.slot[a.wslot] + (size_t)v * W;
-          u64* __restrict__ xrow = a.frx_next ? a.frx_next + (size_t)v * W : nullptr;
-          uint8_t* __restrict__ frow = a.first ? a.first + (size_t)li * (W * 64) : nullptr;
-#pragma unroll 2
-          for (int w = 0; w < W; ++w) {
-            const u64 nw = F.acc[lane][w];
-            const u64 s = srow ? srow[w] : 0ull;   // srow may be drow (in place): read first
-            drow[w] = s | nw;
-            if (xrow) xrow[w] = nw;
-            if (nw) {
-              if (a.digest) dig ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + w), nw);
-              if (frow) set_first_bytes(frow, w, nw, (uint32_t)a.rr);
-            }
-          }
-          a.seenpop[li] = spop + tot;
-          a.sp[v] = (uint8_t)a.wslot;
-          a.ws[v] |= (uint8_t)(1u << a.wslot);
-          if (a.digest) a.digest[li] ^= dig;
-          nbits = tot;
-          nrecv = 1;
-          nwritten = 1;
-          narcs = (u64)(uint32_t)max(a.deg_live[v], 0);
-        }
+      const uint32_t tot = F.tot[lane];
+      nseen = (u64)F.rd[lane];
+      a.fpop_next[v] = tot;
+      if (tot) {
+        a.seenpop[li] = spop + tot;
+        a.sp[v] = (uint8_t)a.wslot;
+        a.ws[v] |= (uint8_t)(1u << a.wslot);
+        if (a.digest) a.digest[li] ^= F.dig[lane];
+        nbits = tot;
+        nrecv = 1;
+        nwritten = 1;
+        narcs = (u64)(uint32_t)max(a.deg_live[v], 0);
       }
     }
     st.add(S_NEW_BITS, wave_sum_u64(nbits));
