@@ -640,12 +640,137 @@ struct FlatLds {
   int8_t rd[64];                // its seen row was read
 };
 
+// one flat pass: the arcs [start, start + sdeg) of every lane's receiver, as
+// one sequence (owner windows of FLAT_CAP positions), OR-ed into F.acc.
+// Returns the rows gathered.
 template <int W, int MODE>
+__device__ __forceinline__ u64 flat_pass(const ExpandArgs& a, FlatLds<W>& F, int lane, int g, int lw,
+                                         uint32_t sdeg, int64_t start, WaveStats& st) {
+  constexpr int RPI = Geo<W>::RPI;
+  constexpr int WPL = Geo<W>::WPL;
+  constexpr int QA = 4;
+  const uint32_t excl = wave_excl_scan_u32(sdeg, lane);
+  const uint32_t incl = excl + sdeg;
+  const uint32_t T = (uint32_t)__shfl((int)incl, 63);
+  const uint32_t vb_lo = (uint32_t)start, vb_hi = (uint32_t)((u64)start >> 32);
+  st.add(S_ARCS, T);
+  u64 gathered = 0;
+  for (uint32_t g0 = 0; g0 < T; g0 += FLAT_CAP) {
+    const uint32_t wn = min((uint32_t)FLAT_CAP, T - g0);
+    // owner table of positions [g0, g0 + wn): start markers, then a forward
+    // fill seeded with the receiver that straddles g0
+    {
+      u64* own8 = reinterpret_cast<u64*>(F.own);
+      own8[lane] = 0xFFFFFFFFFFFFFFFFull;
+      wave_sync_lds();
+      if (sdeg && excl >= g0 && excl < g0 + wn) F.own[excl - g0] = (int8_t)lane;
+      const u64 before = __ballot(sdeg && excl < g0);
+      const int carry_in = before ? 63 - __clzll((long long)before) : -1;
+      wave_sync_lds();
+      const u64 w8 = own8[lane];
+      int run = -1;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int o = (int8_t)((w8 >> (8 * q)) & 0xFF);
+        if (o >= 0) run = o;
+      }
+      int carry = run;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(carry, o);
+        if (lane >= o) carry = max(carry, y);
+      }
+      int cur = __shfl_up(carry, 1);
+      if (lane == 0) cur = carry_in;
+      cur = max(cur, carry_in);
+      u64 out = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int o = (int8_t)((w8 >> (8 * q)) & 0xFF);
+        if (o >= 0) cur = o;
+        out |= (u64)(uint8_t)(int8_t)cur << (8 * q);
+      }
+      own8[lane] = out;
+      wave_sync_lds();
+    }
+    for (uint32_t c0 = 0; c0 < wn; c0 += 64 * QA) {
+      int32_t col[QA];
+      int8_t who[QA];
+#pragma unroll
+      for (int q = 0; q < QA; ++q) {
+        const uint32_t p = c0 + (uint32_t)(q * 64 + lane);
+        const int j = p < wn ? (int)F.own[p] : 0;
+        // shuffles with the whole wave active (bpermute reads every lane)
+        const int64_t b = (int64_t)(((u64)(uint32_t)__shfl((int)vb_hi, j) << 32) |
+                                    (u64)(uint32_t)__shfl((int)vb_lo, j));
+        const uint32_t s = (uint32_t)__shfl((int)excl, j);
+        who[q] = (int8_t)j;
+        col[q] = -1;
+        if (p < wn) col[q] = a.gcol[b + (g0 + p - s)];
+      }
+      u64 raw[QA];   // activity words, all in flight before the first use
+#pragma unroll
+      for (int q = 0; q < QA; ++q) {
+        raw[q] = ~0ull;
+        if constexpr (MODE != SCAN_UNFILTERED)
+          if (col[q] >= 0) raw[q] = a.abits[col[q] >> 6];
+      }
+#pragma unroll
+      for (int q = 0; q < QA; ++q) {
+        const int32_t u = (col[q] >= 0 && ((raw[q] >> (col[q] & 63)) & 1ull)) ? col[q] : -1;
+        const u64 am = __ballot(u >= 0);
+        const int cnt = __popcll(am);
+        if (cnt == 0) continue;
+        if (u >= 0) {
+          const int r = lane_rank(am);
+          F.idx[r] = u;
+          F.vtx[r] = who[q];
+        }
+        wave_sync_lds();
+        gathered += (u64)cnt;
+        for (int k0 = 0; k0 < cnt; k0 += GP_FLAT_ROWS_IN_FLIGHT * RPI) {
+          u64x2 r[GP_FLAT_ROWS_IN_FLIGHT];
+#pragma unroll
+          for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
+            const int k = k0 + g + t * RPI;
+            r[t] = u64x2{0, 0};
+            if (k < cnt) r[t] = load_piece<W>(a.rows, F.idx[k], lw);
+          }
+#pragma unroll
+          for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
+            const int k = k0 + g + t * RPI;
+            if (k < cnt) {
+              u64* dst = &F.acc[F.vtx[k]][lw * WPL];
+              if (r[t].x) atomicOr(dst, r[t].x);
+              if constexpr (WPL == 2) {
+                if (r[t].y) atomicOr(dst + 1, r[t].y);
+              }
+            }
+          }
+        }
+        wave_sync_lds();
+      }
+    }
+  }
+  return gathered;
+}
+
+// early-exit rounds: the first GP_FLAT_EE_PREFIX arcs of every
+// receiver (its biggest neighbours: gather order) go in a first pass, arcs up to
+// GP_FLAT_EE_PREFIX2 in a second; only receivers still missing messages of
+// their component after a pass scan further.
+#ifndef GP_FLAT_EE_PREFIX
+#define GP_FLAT_EE_PREFIX 2
+#endif
+#ifndef GP_FLAT_EE_PREFIX2
+#define GP_FLAT_EE_PREFIX2 0
+#endif
+
+template <int W, int MODE, bool EE>
 __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
   constexpr int RPI = Geo<W>::RPI;
   constexpr int WPL = Geo<W>::WPL;
-  constexpr int QA = 4;
   __shared__ FlatLds<W> s_f[WAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
@@ -655,134 +780,88 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
   ws_zero(st);
   const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
   if (base < a.nloc) {
+    // per-lane state is reloaded (coalesced) where it is needed rather than
+    // kept live across the passes: VGPRs are what bound this kernel's waves
     const int64_t li = base + lane;
-    bool need = false, act = false;
-    u64 sends = 0;
-    uint32_t spop = 0, deg = 0, slot_of = SLOT_NONE;
-    int64_t vb = 0;
-    int v = 0;
-    if (li < a.nloc) {
-      v = (int)(a.vbegin + li);
-      const uint32_t fp = a.fpop[v];
-      act = fp != 0u;
-      if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
-      vb = a.row_ptr[v];
-      const int64_t e = a.row_ptr[v + 1];
-      const bool hub = e - vb > a.hub_thr;   // split over waves by the hub kernels
-      spop = a.seenpop[li];
-      need = !(a.state[v] & ST_DOWN) && spop < a.done_at[v] && !hub && e > vb;
-      if (!need && !hub) a.fpop_next[v] = 0;
-      deg = (uint32_t)(e - vb);
-      slot_of = a.sp[v];
+    const int v = li < a.nloc ? (int)(a.vbegin + li) : 0;
+    u64 needm;
+    {
+      bool need = false, act = false;
+      u64 sends = 0;
+      if (li < a.nloc) {
+        const uint32_t fp = a.fpop[v];
+        act = fp != 0u;
+        if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
+        const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
+        const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
+        need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
+        if (!need && !hub) a.fpop_next[v] = 0;
+      }
+      st.add(S_SENDS, wave_sum_u64(sends));
+      st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
+      needm = __ballot(need);
+      st.add(S_VISITED, (u64)__popcll(needm));
     }
-    st.add(S_SENDS, wave_sum_u64(sends));
-    st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
-    st.add(S_VISITED, (u64)__popcll(__ballot(need)));
+    const bool need = (needm >> lane) & 1ull;
 #pragma unroll
     for (int w = 0; w < W; ++w) F.acc[lane][w] = 0ull;
-    const uint32_t sdeg = need ? deg : 0u;
-    const uint32_t excl = wave_excl_scan_u32(sdeg, lane);
-    const uint32_t incl = excl + sdeg;
-    const uint32_t T = (uint32_t)__shfl((int)incl, 63);
-    const uint32_t vb_lo = (uint32_t)vb, vb_hi = (uint32_t)((u64)vb >> 32);
-    st.add(S_ARCS, T);
+    // one pass, or (early-exit rounds) a prefix pass and a pass over the rest
+    // of the in-lists of the receivers still missing messages
+    constexpr uint32_t K1 = GP_FLAT_EE_PREFIX, K2 = GP_FLAT_EE_PREFIX2;
+    constexpr bool ee = EE && K1 > 0;   // compile-time: the lean kernel keeps its VGPRs
+    constexpr int npass = !ee ? 1 : (K2 > K1 ? 3 : 2);
     u64 gathered = 0;
-    for (uint32_t g0 = 0; g0 < T; g0 += FLAT_CAP) {
-      const uint32_t wn = min((uint32_t)FLAT_CAP, T - g0);
-      // owner table of positions [g0, g0 + wn): start markers, then a forward
-      // fill seeded with the receiver that straddles g0
-      {
-        u64* own8 = reinterpret_cast<u64*>(F.own);
-        own8[lane] = 0xFFFFFFFFFFFFFFFFull;
-        wave_sync_lds();
-        if (sdeg && excl >= g0 && excl < g0 + wn) F.own[excl - g0] = (int8_t)lane;
-        const u64 before = __ballot(sdeg && excl < g0);
-        const int carry_in = before ? 63 - __clzll((long long)before) : -1;
-        wave_sync_lds();
-        const u64 w8 = own8[lane];
-        int run = -1;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int o = (int8_t)((w8 >> (8 * q)) & 0xFF);
-          if (o >= 0) run = o;
-        }
-        int carry = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int y = __shfl_up(carry, o);
-          if (lane >= o) carry = max(carry, y);
-        }
-        int cur = __shfl_up(carry, 1);
-        if (lane == 0) cur = carry_in;
-        cur = max(cur, carry_in);
-        u64 out = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int o = (int8_t)((w8 >> (8 * q)) & 0xFF);
-          if (o >= 0) cur = o;
-          out |= (u64)(uint8_t)(int8_t)cur << (8 * q);
-        }
-        own8[lane] = out;
-        wave_sync_lds();
+    u64 todo = needm;   // receivers of this pass
+#pragma nounroll
+    for (int pass = 0; pass < npass; ++pass) {
+      // this pass covers in-list positions [lo, hi)
+      const uint32_t lo = pass == 0 ? 0u : pass == 1 ? K1 : K2;
+      const uint32_t hi = pass + 1 == npass ? 0xFFFFFFFFu : pass == 0 ? K1 : K2;
+      uint32_t sdeg = 0;
+      int64_t start = 0;
+      if ((todo >> lane) & 1ull) {
+        const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
+        const uint32_t deg = (uint32_t)(e - b);
+        sdeg = deg > lo ? min(deg, hi) - lo : 0u;
+        start = b + lo;
       }
-      for (uint32_t c0 = 0; c0 < wn; c0 += 64 * QA) {
-        int32_t col[QA];
-        int8_t who[QA];
-#pragma unroll
-        for (int q = 0; q < QA; ++q) {
-          const uint32_t p = c0 + (uint32_t)(q * 64 + lane);
-          const int j = p < wn ? (int)F.own[p] : 0;
-          // shuffles with the whole wave active (bpermute reads every lane)
-          const int64_t b = (int64_t)(((u64)(uint32_t)__shfl((int)vb_hi, j) << 32) |
-                                      (u64)(uint32_t)__shfl((int)vb_lo, j));
-          const uint32_t s = (uint32_t)__shfl((int)excl, j);
-          who[q] = (int8_t)j;
-          col[q] = -1;
-          if (p < wn) col[q] = a.gcol[b + (g0 + p - s)];
-        }
-        u64 raw[QA];   // activity words, all in flight before the first use
-#pragma unroll
-        for (int q = 0; q < QA; ++q) {
-          raw[q] = ~0ull;
-          if constexpr (MODE != SCAN_UNFILTERED)
-            if (col[q] >= 0) raw[q] = a.abits[col[q] >> 6];
-        }
-#pragma unroll
-        for (int q = 0; q < QA; ++q) {
-          const int32_t u = (col[q] >= 0 && ((raw[q] >> (col[q] & 63)) & 1ull)) ? col[q] : -1;
-          const u64 am = __ballot(u >= 0);
-          const int cnt = __popcll(am);
-          if (cnt == 0) continue;
-          if (u >= 0) {
-            const int r = lane_rank(am);
-            F.idx[r] = u;
-            F.vtx[r] = who[q];
-          }
-          wave_sync_lds();
-          gathered += (u64)cnt;
-          for (int k0 = 0; k0 < cnt; k0 += GP_FLAT_ROWS_IN_FLIGHT * RPI) {
-            u64x2 r[GP_FLAT_ROWS_IN_FLIGHT];
-#pragma unroll
-            for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
-              const int k = k0 + g + t * RPI;
-              r[t] = u64x2{0, 0};
-              if (k < cnt) r[t] = load_piece<W>(a.rows, F.idx[k], lw);
-            }
-#pragma unroll
-            for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
-              const int k = k0 + g + t * RPI;
-              if (k < cnt) {
-                u64* dst = &F.acc[F.vtx[k]][lw * WPL];
-                if (r[t].x) atomicOr(dst, r[t].x);
-                if constexpr (WPL == 2) {
-                  if (r[t].y) atomicOr(dst + 1, r[t].y);
-                }
-              }
-            }
-          }
-          wave_sync_lds();
+      gathered += flat_pass<W, MODE>(a, F, lane, g, lw, sdeg, start, st);
+      if (pass + 1 == npass) break;
+      // which receivers with arcs left still miss messages of their component?
+      bool longer = false;
+      uint32_t slot_of = SLOT_NONE;
+      int32_t mrow = -1;
+      if ((todo >> lane) & 1ull) {
+        longer = a.row_ptr[v + 1] - a.row_ptr[v] > (int64_t)hi;
+        if (longer) {
+          slot_of = a.sp[v];
+          mrow = a.midx[v];
         }
       }
+      const u64 longm = __ballot(longer);
+      wave_sync_lds();
+#pragma nounroll
+      for (int r0 = 0; r0 < 64; r0 += RPI) {
+        const int r = r0 + g;
+        const uint32_t rslot = (uint32_t)__shfl((int)slot_of, r);
+        const int rv = __shfl(v, r);
+        const int32_t rm = __shfl(mrow, r);
+        bool miss = false;
+        if ((longm >> r) & 1ull) {
+          u64x2 accp;
+          accp.x = F.acc[r][lw * WPL];
+          accp.y = 0;
+          if constexpr (WPL == 2) accp.y = F.acc[r][lw * WPL + 1];
+          const u64x2 sv = rslot != SLOT_NONE ? load_piece<W>(a.slot[rslot], rv, lw) : u64x2{0, 0};
+          const u64x2 cm = load_piece<W>(a.cmask, rm, lw);
+          const u64x2 m = cm & ~(sv | accp);
+          miss = (m.x | m.y) != 0ull;
+        }
+        miss = group_or<LPR>(miss);
+        if (lw == 0) F.rd[r] = (int8_t)miss;
+      }
+      wave_sync_lds();
+      todo = __ballot(((longm >> lane) & 1ull) && F.rd[lane]);
     }
     st.add(S_GATHERED, gathered);
     st.add(S_ROW_BYTES, gathered * (u64)(8 * W));
@@ -791,7 +870,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
     // writes nothing.  Per-receiver words go to F.tot / F.dig, then one
     // coalesced commit with one receiver per lane.
     wave_sync_lds();
-    const u64 needm = __ballot(need);
+    const uint32_t slot_of = need ? a.sp[v] : SLOT_NONE;
     for (int r0 = 0; r0 < 64; r0 += RPI) {
       const int r = r0 + g;
       const uint32_t rslot = (uint32_t)__shfl((int)slot_of, r);
@@ -835,7 +914,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       nseen = (u64)F.rd[lane];
       a.fpop_next[v] = tot;
       if (tot) {
-        a.seenpop[li] = spop + tot;
+        a.seenpop[li] += tot;
         a.sp[v] = (uint8_t)a.wslot;
         a.ws[v] |= (uint8_t)(1u << a.wslot);
         if (a.digest) a.digest[li] ^= F.dig[lane];
@@ -1610,10 +1689,14 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
     const dim3 grid(grid_for(a.nloc, per_block));
     if constexpr (W <= 32) {
-      if (mode == SCAN_UNFILTERED)
-        hipLaunchKernelGGL((k_expand_flat<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
-      else
-        hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+      const bool ee = a.early_exit != 0 && GP_FLAT_EE_PREFIX > 0;
+      if (mode == SCAN_UNFILTERED) {
+        if (ee) hipLaunchKernelGGL((k_expand_flat<W, SCAN_UNFILTERED, true>), grid, dim3(BLOCK), 0, c->stream, a);
+        else hipLaunchKernelGGL((k_expand_flat<W, SCAN_UNFILTERED, false>), grid, dim3(BLOCK), 0, c->stream, a);
+      } else {
+        if (ee) hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED, true>), grid, dim3(BLOCK), 0, c->stream, a);
+        else hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED, false>), grid, dim3(BLOCK), 0, c->stream, a);
+      }
     }
   } else if (a.nloc > 0) {
     const dim3 grid(grid_for(a.nloc, per_block));
