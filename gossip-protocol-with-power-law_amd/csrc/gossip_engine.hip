@@ -629,15 +629,20 @@ constexpr int FLAT_CAP = 512;   // arc positions per owner window
 #ifndef GP_FLAT_ROWS_IN_FLIGHT
 #define GP_FLAT_ROWS_IN_FLIGHT 2
 #endif
+// receivers per wave: 64, or 32 at W = 32 so that the LDS accumulators (8 KB
+// per wave) leave room for 4 blocks per CU
+template <int W>
+struct FlatNR { static constexpr int value = W >= 32 ? 32 : 64; };
 template <int W>
 struct FlatLds {
-  u64 acc[64][W];               // OR accumulators of the wave's 64 receivers
+  static constexpr int NR = FlatNR<W>::value;
+  u64 acc[NR][W];               // OR accumulators of the wave's NR receivers
   int32_t idx[64];              // active neighbours of one chunk
   int8_t vtx[64];               // their receiver (lane) in the wave
   int8_t own[FLAT_CAP];         // receiver lane owning each arc position of the window
-  uint32_t tot[64];             // receiver side: new bits of receiver k
-  u64 dig[64];                  // its digest terms
-  int8_t rd[64];                // its seen row was read
+  uint32_t tot[NR];             // receiver side: new bits of receiver k
+  u64 dig[NR];                  // its digest terms
+  int8_t rd[NR];                // its seen row was read
 };
 
 // one flat pass: the arcs [start, start + sdeg) of every lane's receiver, as
@@ -776,19 +781,21 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
   FlatLds<W>& F = s_f[wib];
+  constexpr int NR = FlatNR<W>::value;
   WaveStats st;
   ws_zero(st);
-  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
+  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * NR;
   if (base < a.nloc) {
     // per-lane state is reloaded (coalesced) where it is needed rather than
     // kept live across the passes: VGPRs are what bound this kernel's waves
     const int64_t li = base + lane;
-    const int v = li < a.nloc ? (int)(a.vbegin + li) : 0;
+    const bool mine = lane < NR && li < a.nloc;   // lane = receiver
+    const int v = mine ? (int)(a.vbegin + li) : 0;
     u64 needm;
     {
       bool need = false, act = false;
       u64 sends = 0;
-      if (li < a.nloc) {
+      if (mine) {
         const uint32_t fp = a.fpop[v];
         act = fp != 0u;
         if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
@@ -803,8 +810,10 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       st.add(S_VISITED, (u64)__popcll(needm));
     }
     const bool need = (needm >> lane) & 1ull;
+    if (lane < NR) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) F.acc[lane][w] = 0ull;
+      for (int w = 0; w < W; ++w) F.acc[lane][w] = 0ull;
+    }
     // one pass, or (early-exit rounds) a prefix pass and a pass over the rest
     // of the in-lists of the receivers still missing messages
     constexpr uint32_t K1 = GP_FLAT_EE_PREFIX, K2 = GP_FLAT_EE_PREFIX2;
@@ -841,7 +850,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       const u64 longm = __ballot(longer);
       wave_sync_lds();
 #pragma nounroll
-      for (int r0 = 0; r0 < 64; r0 += RPI) {
+      for (int r0 = 0; r0 < NR; r0 += RPI) {
         const int r = r0 + g;
         const uint32_t rslot = (uint32_t)__shfl((int)slot_of, r);
         const int rv = __shfl(v, r);
@@ -871,7 +880,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
     // coalesced commit with one receiver per lane.
     wave_sync_lds();
     const uint32_t slot_of = need ? a.sp[v] : SLOT_NONE;
-    for (int r0 = 0; r0 < 64; r0 += RPI) {
+    for (int r0 = 0; r0 < NR; r0 += RPI) {
       const int r = r0 + g;
       const uint32_t rslot = (uint32_t)__shfl((int)slot_of, r);
       const int rv = __shfl(v, r);
@@ -1687,7 +1696,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   const int mode = a.unfiltered ? SCAN_UNFILTERED : SCAN_FILTERED;
   (void)hipEventRecord(c->ev[4], c->stream);
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
-    const dim3 grid(grid_for(a.nloc, per_block));
+    const dim3 grid(grid_for(a.nloc, (int64_t)WAVES * FlatNR<W>::value));
     if constexpr (W <= 32) {
       const bool ee = a.early_exit != 0 && GP_FLAT_EE_PREFIX > 0;
       if (mode == SCAN_UNFILTERED) {

@@ -100,7 +100,7 @@ def test_c2_ba_10k_64(pkg, oracle, mode):
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
-@pytest.mark.parametrize("m", [1, 10, 63, 64, 65, 130, 300, 1000, 4096])
+@pytest.mark.parametrize("m", [1, 10, 63, 64, 65, 130, 300, 1000, 2000, 4096])
 def test_message_widths(pkg, oracle, m, mode):
     push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.barabasi_albert(1500, 3, seed=m)
