@@ -233,7 +233,11 @@ struct WaveLds {
   u64 dig[64];          // k_expand: digest terms of vertex k
   int64_t rp[65];       // k_expand: row_ptr of the wave's vertices (rp[k], rp[k + 1])
   int32_t mi[64];       // k_expand: component-mask row of vertex k (early-exit rounds)
+  int32_t pre[64][8];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
+  uint8_t np[64];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
 };
+constexpr int PRE_IDS = 8;       // active neighbours kept per prefiltered vertex
+constexpr int PRE_MAX_DEG = 16;  // in-degree up to which the lane phase probes
 
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -293,7 +297,7 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
 // scan modes of a pull round (compile-time): the per-arc activity probe, the
 // per-arc activity mask built by k_arcmask before the round, or no check at all
 // (unfiltered dense rounds)
-enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2 };
+enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PRE = 3 };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
@@ -340,8 +344,8 @@ __device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
 #define GP_WORD_SKIP 1
 #endif
 template <int W>
-__device__ __forceinline__ bool gather_rows(const ExpandArgs& a, WaveLds& L, int cnt, int g, int lw, u64x2& acc,
-                                            WaveStats& st, bool ee, u64x2 want) {
+__device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
+                                            u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
   constexpr int RPI = Geo<W>::RPI;
   bool live = true;   // this lane's words still miss messages
   if (GP_WORD_SKIP && ee) {
@@ -356,7 +360,7 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, WaveLds& L, int
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
       const int k = k0 + g + q * RPI;
       r[q] = u64x2{0, 0};
-      if (k < cnt && live) r[q] = load_piece<W>(a.rows, L.idx[k], lw);
+      if (k < cnt && live) r[q] = load_piece<W>(a.rows, idx[k], lw);
     }
 #pragma unroll
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
@@ -430,7 +434,7 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
       cnt = stage_pass(L, ent);
       if (cnt == 0) continue;
     }
-    const bool stop = gather_rows<W>(a, L, cnt, g, lw, acc, st, ee, want);
+    const bool stop = gather_rows<W>(a, L.idx, cnt, g, lw, acc, st, ee, want);
     wave_sync_lds();
     if (stop) break;
   }
@@ -570,6 +574,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     bool need = false, act = false;
     u64 sends = 0;
     uint32_t slot_of = SLOT_NONE;
+    uint32_t pre_arcs = 0;   // SCAN_PRE: arcs the lane phase scanned
     if (li < a.nloc) {
       const int v = (int)(a.vbegin + li);
       const uint32_t fp = a.fpop[v];
@@ -581,10 +586,46 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
       need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
       if constexpr (MODE == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
+      if constexpr (MODE == SCAN_PRE) {
+        // sparse filtered rounds: every lane probes the in-list of its own
+        // vertex (up to PRE_MAX_DEG arcs, all loads in flight together), so the
+        // wave's serial loop skips vertices with no active in-neighbour and
+        // starts the others at their rows
+        uint32_t np = 0xFFu;
+        if (need && e - b <= PRE_MAX_DEG) {
+          const int deg = (int)(e - b);
+          uint32_t cnt = 0;
+#pragma unroll
+          for (int h = 0; h < PRE_MAX_DEG / PRE_IDS; ++h) {
+            if (h * PRE_IDS < deg) {
+              int32_t c[PRE_IDS];
+              u64 w[PRE_IDS];
+#pragma unroll
+              for (int q = 0; q < PRE_IDS; ++q) c[q] = h * PRE_IDS + q < deg ? a.gcol[b + h * PRE_IDS + q] : -1;
+#pragma unroll
+              for (int q = 0; q < PRE_IDS; ++q) w[q] = c[q] >= 0 ? a.abits[c[q] >> 6] : 0ull;
+#pragma unroll
+              for (int q = 0; q < PRE_IDS; ++q) {
+                if (c[q] >= 0 && ((w[q] >> (c[q] & 63)) & 1ull)) {
+                  if (cnt < (uint32_t)PRE_IDS) L.pre[lane][cnt] = c[q];
+                  ++cnt;
+                }
+              }
+            }
+          }
+          if (cnt <= (uint32_t)PRE_IDS) {
+            np = cnt;
+            pre_arcs = (uint32_t)deg;
+          }
+          if (cnt == 0) need = false;
+        }
+        L.np[lane] = (uint8_t)np;
+      }
       if (!need && !hub) a.fpop_next[v] = 0;
       slot_of = a.sp[v];
       if (a.early_exit && need) L.mi[lane] = a.midx[v];
     }
+    if constexpr (MODE == SCAN_PRE) st.add(S_ARCS, (u64)wave_sum_u32(pre_arcs));
     st.add(S_SENDS, wave_sum_u64(sends));
     st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
     st.add(S_VISITED, (u64)__popcll(__ballot(need)));
@@ -605,7 +646,13 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         if (sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
         want = early_exit_target<W>(a, v, L, g, lw, sv_slot, L.mi[k]);
       }
-      gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
+      if constexpr (MODE == SCAN_PRE) {
+        const uint32_t np = L.np[k];
+        if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);
+        else gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
+      } else {
+        gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
+      }
       reduce_slots<W>(acc);
       finish_row<W, true>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot, k);
     }
@@ -1713,6 +1760,8 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
     else if (masked)
       hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(BLOCK), 0, c->stream, a);
+    else if (c->prefilter_now)
+      hipLaunchKernelGGL((k_expand<W, SCAN_PRE>), grid, dim3(BLOCK), 0, c->stream, a);
     else
       hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
   }
@@ -1752,6 +1801,9 @@ static int launch_expand(Ctx* c) {
   // first (pays once the probes are many: senders >= arc_mask_permille of n)
   c->arc_mask_now = !c->mode_push && !c->unfiltered_now && c->cfg.arc_mask_permille > 0 &&
                     senders * 1000.0 >= (double)c->cfg.arc_mask_permille * (double)c->n;
+  // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
+  c->prefilter_now = !c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.prefilter_pct > 0 &&
+                     senders * 100.0 < (double)c->cfg.prefilter_pct * (double)c->n;
   ExpandArgs a{};
   fill_expand(c, a);
   a.unfiltered = c->unfiltered_now ? 1 : 0;
@@ -2017,7 +2069,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->push_ratio = 400.0;   // push when sender arcs <= nnz / 400
   cfg->early_exit = 1;
   cfg->arc_mask_permille = 0;   // per-arc mask off: its build costs what it saves
-  cfg->reserved1 = 0;
+  cfg->prefilter_pct = 20;
   cfg->unfiltered_pct = 90;
   cfg->msg_word_base = 0;
   cfg->flat_max_words = 16;
@@ -2081,7 +2133,7 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->hub_threshold < 64) return set_error(GP_EINVAL, "hub_threshold must be >= 64");
   if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
   if (cfg->msg_word_base < 0) return set_error(GP_EINVAL, "msg_word_base < 0");
-  if (cfg->reserved1) return set_error(GP_EINVAL, "reserved config fields must be 0");
+  if (cfg->prefilter_pct < 0) return set_error(GP_EINVAL, "prefilter_pct < 0");
   if (cfg->arc_mask_permille < 0) return set_error(GP_EINVAL, "arc_mask_permille < 0");
   GP_HIP(hipSetDevice(c->device));
   const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
@@ -2451,7 +2503,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->next_arcs = h[S_NEXT_ARCS];
     out->row_bytes = h[S_ROW_BYTES];
     out->mode = c->mode_push ? 1 : 0;
-    out->scan = c->mode_push ? 0 : c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : 0;
+    out->scan = c->mode_push ? 0 : c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : c->prefilter_now ? 3 : 0;
     out->kernel_ms = 0.0;
     if (!c->mode_push && c->nloc() > 0) {
       float kms = 0.f;

@@ -101,6 +101,7 @@ struct Ctx {
   u64 prev_receivers = 0;           // receivers of the last round (global)
   bool unfiltered_now = false;      // this round's pull skips the activity check
   bool arc_mask_now = false;        // this round's filtered pull reads the per-arc mask
+  bool prefilter_now = false;       // this round's filtered pull probes low-degree in-lists lane-parallel
   int64_t inj_groups_at(int32_t r) const {
     auto it = inject.find(r);
     return it == inject.end() ? 0 : it->second.cnt;

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 8
+#define GP_ABI_VERSION 9
 
 typedef struct gp_ctx gp_ctx;
 
@@ -79,7 +79,8 @@ typedef struct gp_round_stats {
   int32_t mode;             /* 0 = pull expansion, 1 = push expansion                 */
   int32_t scan;             /* pull arc check: 0 = activity-bitmap probe per arc,
                                1 = per-arc activity mask built first (§3.2),
-                               2 = none, every in-neighbour row read (§3.4)          */
+                               2 = none, every in-neighbour row read (§3.4),
+                               3 = probe, low-degree in-lists prefiltered (§3.2)     */
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
@@ -109,8 +110,9 @@ typedef struct gp_config {
   int32_t arc_mask_permille;   /* filtered pull rounds with >= this many senders per 1000
                                   vertices build the per-arc activity mask first
                                   (0 = always probe per arc)           */
-  int32_t reserved1;           /* must be 0 (was an id-list frontier-row format; the pull
-                                  now reads Message-List slots)         */
+  int32_t prefilter_pct;       /* filtered pull rounds with < this % of vertices sending
+                                  probe the in-lists of receivers of in-degree <= 16
+                                  lane-parallel first (0 = never)       */
   int32_t unfiltered_pct;      /* pull without the per-arc activity check when >= this %
                                   of vertices are senders (0 = never)   */
   int32_t msg_word_base;       /* message shards: this context's message k
