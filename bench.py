@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--arc-mask-permille", type=int, default=0,
                     help="filtered pull rounds with >= this many senders per 1000 vertices build "
                          "the per-arc activity mask first (0 = always probe per arc)")
+    ap.add_argument("--compact-rows", type=int, default=0,
+                    help="1: sparse 64-word rounds gather compact Message-Lists (DESIGN.md §3.2)")
+    ap.add_argument("--prefilter-pct", type=int, default=20)
     ap.add_argument("--flat-max-words", type=int, default=16,
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -135,7 +138,8 @@ def main():
                            push_ratio=args.push_ratio,
                            early_exit=args.early_exit,
                            unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words,
-                           arc_mask_permille=args.arc_mask_permille)
+                           arc_mask_permille=args.arc_mask_permille, compact_rows=args.compact_rows,
+                           prefilter_pct=args.prefilter_pct)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()

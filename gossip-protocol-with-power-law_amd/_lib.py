@@ -79,6 +79,7 @@ class Config(ctypes.Structure):
         ("early_exit", ctypes.c_int32),
         ("arc_mask_permille", ctypes.c_int32),
         ("prefilter_pct", ctypes.c_int32),
+        ("compact_rows", ctypes.c_int32),
         ("unfiltered_pct", ctypes.c_int32),
         ("msg_word_base", ctypes.c_int32),
         ("flat_max_words", ctypes.c_int32),
@@ -116,7 +117,7 @@ SIGNATURES = {
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
 }
 
-ABI_VERSION = 9   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 10   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

@@ -177,6 +177,11 @@ struct ExpandArgs {
   int32_t early_exit;                  // this round scans with the coverage check
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
+  const u64* __restrict__ cmk;         // compact-list masks of this round's senders (or null):
+                                       //   0 = not a sender, CML_DENSE = full row, else the mask
+  const u64* __restrict__ cml;         // their compact records
+  u64* __restrict__ cmk_next;          // masks / records the receivers write (or null)
+  u64* __restrict__ cml_next;
   const uint32_t* __restrict__ done_at;// |messages of v's component|: seenpop == done_at -> done
   uint32_t* __restrict__ fpop_next;
   u64* __restrict__ frx;               // exact frontier rows of round r (track_msg_forwards only)
@@ -211,6 +216,15 @@ struct ExpandArgs {
 
 constexpr uint8_t SLOT_NONE = 0xFF;
 
+// compact Message-Lists (W = 64): per vertex a mask word
+// (cmk: bit w = word w of its Message-List is nonzero; 0 = not a sender this
+// round; CML_DENSE = more than CML_WORDS nonzero words, read the full row) and
+// a 128-B record holding the nonzero words in order.  Sparse rounds probe the
+// mask instead of the activity bitmap and gather one line per sender instead
+// of four.
+constexpr int CML_WORDS = 16;
+constexpr u64 CML_DENSE = ~0ull;
+
 // occupancy target of k_expand (waves per SIMD; 0 = compiler's choice)
 #ifndef GP_EXPAND_WAVES
 #define GP_EXPAND_WAVES 0
@@ -233,6 +247,8 @@ struct WaveLds {
   u64 dig[64];          // k_expand: digest terms of vertex k
   int64_t rp[65];       // k_expand: row_ptr of the wave's vertices (rp[k], rp[k + 1])
   int32_t mi[64];       // k_expand: component-mask row of vertex k (early-exit rounds)
+  u64 msk[64];          // compact-row rounds: the staged senders' record masks
+  u64 cm[64];           // compact-row rounds: mask word of the wave's vertex k (committed)
   int32_t pre[64][8];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
   uint8_t np[64];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
 };
@@ -297,7 +313,8 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
 // scan modes of a pull round (compile-time): the per-arc activity probe, the
 // per-arc activity mask built by k_arcmask before the round, or no check at all
 // (unfiltered dense rounds)
-enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PRE = 3 };
+enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PRE = 3,
+                SCAN_CML = 4 /* flag: read / write compact Message-Lists (W = 64) */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
@@ -325,7 +342,7 @@ __device__ __forceinline__ bool mask_any(const u64* __restrict__ amask, int64_t 
 // neighbour u if its row is read this round, else -1
 template <int MODE>
 __device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
-  if constexpr (MODE == SCAN_UNFILTERED) {
+  if constexpr ((MODE & 3) == SCAN_UNFILTERED) {
     return u;
   } else {
     return ((a.abits[u >> 6] >> (u & 63)) & 1ull) ? u : -1;
@@ -380,6 +397,57 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* 
   return false;
 }
 
+// compact-row rounds: the staged senders' record masks into L.msk (one
+// instruction for the pass), and the record/row bytes they stand for
+template <int W>
+__device__ __forceinline__ void stage_masks(const ExpandArgs& a, WaveLds& L, const int32_t* idx, int cnt,
+                                            WaveStats& st) {
+  const int lane = threadIdx.x & 63;
+  u64 bytes = 0;
+  if (lane < cnt) {
+    const u64 m = a.cmk[idx[lane]];
+    L.msk[lane] = m;
+    bytes = m == CML_DENSE ? (u64)(8 + 8 * W) : (u64)(8 + 8 * __popcll(m));
+  }
+  st.add(S_ROW_BYTES, wave_sum_u64(bytes));
+  wave_sync_lds();
+}
+
+// gather_rows over compact records (no early exit: sparse rounds only).  Lane
+// (g, lw) holds words 2lw, 2lw + 1: from a compact record it loads the packed
+// entries of those words if they are nonzero, from a dense sender its piece.
+template <int W>
+__device__ __forceinline__ void gather_rows_cml(const ExpandArgs& a, const WaveLds& L, const int32_t* idx, int cnt,
+                                                int g, int lw, u64x2& acc, WaveStats& st) {
+  constexpr int RPI = Geo<W>::RPI;
+  static_assert(W == 64, "compact records hold 64-word rows");
+  const int w0 = 2 * lw;
+  const u64 below = (1ull << w0) - 1ull;   // words below w0
+  for (int k0 = 0; k0 < cnt; k0 += GP_ROWS_IN_FLIGHT * RPI) {
+    u64x2 r[GP_ROWS_IN_FLIGHT];
+#pragma unroll
+    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
+      const int k = k0 + g + q * RPI;
+      r[q] = u64x2{0, 0};
+      if (k < cnt) {
+        const int32_t u = idx[k];
+        const u64 m = L.msk[k];
+        if (m == CML_DENSE) {
+          r[q] = load_piece<W>(a.rows, u, lw);
+        } else {
+          const u64* rec = a.cml + (size_t)u * CML_WORDS;
+          const int p = __popcll(m & below);
+          if ((m >> w0) & 1ull) r[q].x = rec[p];
+          if ((m >> (w0 + 1)) & 1ull) r[q].y = rec[p + (int)((m >> w0) & 1ull)];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
+    st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
+  }
+}
+
 // stage one pass of probed neighbours (e: this lane's entry, -1 = none) in
 // LDS; returns their count
 __device__ __forceinline__ int stage_pass(WaveLds& L, int32_t e) {
@@ -421,7 +489,32 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
     const int n = (int)min((int64_t)64, e - j0);
     st.add(S_ARCS, n);
     int cnt;
-    if constexpr (MODE == SCAN_MASKED) {
+    if constexpr (W == 64 && (MODE & SCAN_CML) != 0) {
+      if (a.cmk) {   // sparse round: the mask array is the probe (no early exit here)
+        int32_t u = -1;
+        u64 m = 0;
+        if (lane < n) {
+          u = a.gcol[j0 + lane];
+          m = a.cmk[u];
+        }
+        const u64 am = __ballot(m != 0ull);
+        u64 bytes = 0;
+        if (m) {
+          const int r = lane_rank(am);
+          L.idx[r] = u;
+          L.msk[r] = m;
+          bytes = m == CML_DENSE ? (u64)(8 * W) : (u64)(8 * __popcll(m));
+        }
+        st.add(S_ROW_BYTES, wave_sum_u64(bytes));
+        wave_sync_lds();
+        cnt = __popcll(am);
+        if (cnt == 0) continue;
+        gather_rows_cml<W>(a, L, L.idx, cnt, g, lw, acc, st);
+        wave_sync_lds();
+        continue;
+      }
+    }
+    if constexpr ((MODE & 3) == SCAN_MASKED) {
       // the mask names the active arcs: column ids of the others are not loaded
       const u64 win = mask_window(a.amask, j0, n);
       if (win == 0ull) continue;
@@ -459,6 +552,32 @@ __device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int w
   }
 }
 
+// bit i of x -> bit 2i
+__device__ __forceinline__ u64 spread32(u64 x) {
+  x &= 0xFFFFFFFFull;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+// the compact record of a 64-word Message-List held as (g, lw) pieces by the
+// group-0 lanes (W = 64: lanes 0..31, words 2lw and 2lw + 1)
+// returns the vertex's mask word (uniform)
+__device__ __forceinline__ u64 write_cml(u64* __restrict__ cml, int v, int g, int lw, u64x2 row) {
+  const u64 bx = __ballot(g == 0 && row.x != 0ull), by = __ballot(g == 0 && row.y != 0ull);
+  const u64 m = spread32(bx) | (spread32(by) << 1);
+  if (__popcll(m) > CML_WORDS) return CML_DENSE;
+  u64* rec = cml + (size_t)v * CML_WORDS;
+  if (g == 0) {
+    const int p = __popcll(m & ((1ull << (2 * lw)) - 1ull));
+    if (row.x) rec[p] = row.x;
+    if (row.y) rec[p + (row.x ? 1 : 0)] = row.y;
+  }
+  return m;
+}
+
 // receiver side of vertex v (local index i): new = acc & ~seen; write the new
 // seen row to slot wslot, counters.  have_sv: the seen row is parked in L.seen
 // (early exit), else it is loaded here from slot sv_slot.
@@ -466,14 +585,17 @@ __device__ __forceinline__ void set_first_bytes(uint8_t* __restrict__ row, int w
 // go to L.tot/L.dig[k] and the wave commits them for its 64 vertices at once,
 // coalesced, after its loop -- one scattered read-modify-write chain less per
 // receiver, and whole cache lines instead of 1-8 byte pieces.
-template <int W, bool DEFER = false>
+template <int W, bool DEFER = false, bool CMLW = true>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
                                            int g, int lw, WaveStats& st, WaveLds& L, bool have_sv,
                                            uint32_t sv_slot, int k = 0) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
-    if (!DEFER && lane == 0) a.fpop_next[v] = 0;
+    if (!DEFER && lane == 0) {
+      a.fpop_next[v] = 0;
+      if (CMLW && a.cmk_next) a.cmk_next[v] = 0;
+    }
     return;
   }
   if (!have_sv && sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
@@ -490,8 +612,15 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   const uint32_t pc = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
   const uint32_t tot = wave_sum_u32(pc);
   if (tot == 0) {
-    if (!DEFER && lane == 0) a.fpop_next[v] = 0;
+    if (!DEFER && lane == 0) {
+      a.fpop_next[v] = 0;
+      if (CMLW && a.cmk_next) a.cmk_next[v] = 0;
+    }
     return;
+  }
+  u64 cm = 0;
+  if constexpr (W == 64 && CMLW) {
+    if (a.cml_next) cm = write_cml(a.cml_next, v, g, lw, sv | nw);
   }
   if (g == 0) {
     store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);   // the whole row: the slot may hold an older one
@@ -516,9 +645,13 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
     }
   }
   if (DEFER) {
-    if (lane == 0) L.tot[k] = tot;
+    if (lane == 0) {
+      L.tot[k] = tot;
+      if (CMLW) L.cm[k] = cm;
+    }
   } else {
     if (lane == 0) {
+      if (CMLW && a.cmk_next) a.cmk_next[v] = cm;
       a.fpop_next[v] = tot;
       a.seenpop[i] += tot;
       a.sp[v] = (uint8_t)a.wslot;
@@ -542,6 +675,7 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, WaveLds& L,
     const int v = (int)(a.vbegin + li);
     const uint32_t tot = L.tot[lane];
     a.fpop_next[v] = tot;
+    if (a.cmk_next) a.cmk_next[v] = tot ? L.cm[lane] : 0ull;
     if (tot) {
       a.seenpop[li] += tot;
       a.sp[v] = (uint8_t)a.wslot;
@@ -585,8 +719,8 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       if (lane == 63 || li + 1 == a.nloc) L.rp[lane + 1] = e;
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
       need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
-      if constexpr (MODE == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
-      if constexpr (MODE == SCAN_PRE) {
+      if constexpr ((MODE & 3) == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
+      if constexpr ((MODE & 3) == SCAN_PRE) {
         // sparse filtered rounds: every lane probes the in-list of its own
         // vertex (up to PRE_MAX_DEG arcs, all loads in flight together), so the
         // wave's serial loop skips vertices with no active in-neighbour and
@@ -621,11 +755,15 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         }
         L.np[lane] = (uint8_t)np;
       }
-      if (!need && !hub) a.fpop_next[v] = 0;
+      if (!need && !hub) {
+        a.fpop_next[v] = 0;
+        if constexpr ((MODE & SCAN_CML) != 0)
+          if (a.cmk_next) a.cmk_next[v] = 0ull;
+      }
       slot_of = a.sp[v];
       if (a.early_exit && need) L.mi[lane] = a.midx[v];
     }
-    if constexpr (MODE == SCAN_PRE) st.add(S_ARCS, (u64)wave_sum_u32(pre_arcs));
+    if constexpr ((MODE & 3) == SCAN_PRE) st.add(S_ARCS, (u64)wave_sum_u32(pre_arcs));
     st.add(S_SENDS, wave_sum_u64(sends));
     st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
     st.add(S_VISITED, (u64)__popcll(__ballot(need)));
@@ -646,15 +784,25 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         if (sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
         want = early_exit_target<W>(a, v, L, g, lw, sv_slot, L.mi[k]);
       }
-      if constexpr (MODE == SCAN_PRE) {
+      if constexpr ((MODE & 3) == SCAN_PRE) {
         const uint32_t np = L.np[k];
-        if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);
+        bool done = false;
+        if constexpr (W == 64 && (MODE & SCAN_CML) != 0) {
+          if (np != 0xFFu && np && a.cml) {
+            stage_masks<W>(a, L, L.pre[k], (int)np, st);
+            gather_rows_cml<W>(a, L, L.pre[k], (int)np, g, lw, acc, st);
+            wave_sync_lds();
+            done = true;
+          }
+        }
+        if (done) {
+        } else if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);
         else gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       } else {
         gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       }
       reduce_slots<W>(acc);
-      finish_row<W, true>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot, k);
+      finish_row<W, true, (MODE & SCAN_CML) != 0>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot, k);
     }
     commit_vertices(a, L, li, need, st);
   }
@@ -1033,7 +1181,10 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
     const int v = a.hubs[h];
     const int64_t i = v - a.vbegin;
     if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= a.done_at[v]) {
-      if (lane == 0) a.fpop_next[v] = 0;
+      if (lane == 0) {
+        a.fpop_next[v] = 0;
+        if (a.cmk_next) a.cmk_next[v] = 0ull;
+      }
     } else {
       st.add(S_VISITED, 1);
       u64x2 acc = {0, 0};
@@ -1251,7 +1402,7 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
       store_piece<W>(a.acc, v, lw, u64x2{0, 0});
     }
     st.add(S_VISITED, 1);
-    finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
+    finish_row<W, false, false>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
   }
   flush_stats(st, a.partial);
 }
@@ -1396,6 +1547,7 @@ struct InjectArgs {
   uint8_t* __restrict__ ws;
   uint32_t* __restrict__ fpop;
   u64* __restrict__ frx;               // exact frontier rows (track_msg_forwards only)
+  u64* __restrict__ cmk;               // compact-list masks of slot r & 1 (or null)
   uint32_t* __restrict__ seenpop;
   uint8_t* __restrict__ first;
   u64* __restrict__ digest;
@@ -1434,6 +1586,7 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
         a.slot[a.rslot][(size_t)o * a.words + lane] = s | b;
         if (a.frx) a.frx[(size_t)o * a.words + lane] = f | b;
       }
+      if (a.cmk && lane == 0) a.cmk[o] = CML_DENSE;   // a sender this round, read as a full row
       const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
       if (lane == 0) {
         a.fpop[o] = fp + nb;
@@ -1673,6 +1826,10 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.fpop = c->d_fpop[c->cur];
   a.abits = c->d_abits;
   a.amask = c->d_amask;
+  a.cmk = c->cml_read_now ? c->d_cmk[c->cur] : nullptr;
+  a.cml = c->cml_read_now ? c->d_cml[c->cur] : nullptr;
+  a.cmk_next = c->cml_write_now ? c->d_cmk[c->cur ^ 1] : nullptr;
+  a.cml_next = c->cml_write_now ? c->d_cml[c->cur ^ 1] : nullptr;
   a.frx = c->d_frx[0] ? c->d_frx[c->cur] : nullptr;
   a.frx_next = c->d_frx[0] ? c->d_frx[c->cur ^ 1] : nullptr;
   a.done_at = c->d_done_at;
@@ -1760,7 +1917,14 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
     else if (masked)
       hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(BLOCK), 0, c->stream, a);
-    else if (c->prefilter_now)
+    else if (W == 64 && (a.cmk || a.cmk_next)) {   // compact Message-Lists read and / or written
+      if constexpr (W == 64) {
+        if (c->prefilter_now)
+          hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_CML>), grid, dim3(BLOCK), 0, c->stream, a);
+        else
+          hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_CML>), grid, dim3(BLOCK), 0, c->stream, a);
+      }
+    } else if (c->prefilter_now)
       hipLaunchKernelGGL((k_expand<W, SCAN_PRE>), grid, dim3(BLOCK), 0, c->stream, a);
     else
       hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
@@ -1801,6 +1965,18 @@ static int launch_expand(Ctx* c) {
   // first (pays once the probes are many: senders >= arc_mask_permille of n)
   c->arc_mask_now = !c->mode_push && !c->unfiltered_now && c->cfg.arc_mask_permille > 0 &&
                     senders * 1000.0 >= (double)c->cfg.arc_mask_permille * (double)c->n;
+  // compact Message-Lists (W = 64): written while the rows are sparse (last
+  // round's receivers got <= CML_AVG_BITS new bits on average), read by a
+  // filtered pull whose senders all wrote theirs in the previous round
+  {
+    constexpr double CML_AVG_BITS = 16.0;
+    const bool ok = c->d_cml[0] != nullptr && c->words == 64 && !c->mode_push;
+    const bool sparse = (double)c->prev_new_bits <= CML_AVG_BITS * (double)std::max<u64>(c->prev_receivers, 1);
+    // (not with liveness: a crash zeroes fpop, not the mask word)
+    c->cml_read_now = ok && sparse && c->cml_written_prev && !c->unfiltered_now && !c->arc_mask_now &&
+                      !c->liveness_active;
+    c->cml_write_now = ok && sparse && !c->unfiltered_now && !c->arc_mask_now;   // the kernels that write them
+  }
   // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
   c->prefilter_now = !c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.prefilter_pct > 0 &&
                      senders * 100.0 < (double)c->cfg.prefilter_pct * (double)c->n;
@@ -1899,7 +2075,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_sp); dfree(&c->d_ws);
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
@@ -1956,6 +2132,18 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_deg_live, na));
   GP_TRY(dalloc(&c->d_cand, na));
   GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
+  // compact Message-Lists: 2 x 128 B per vertex, single-rank W = 64 runs only
+  if (c->cfg.compact_rows && W == 64 && c->nranks == 1) {
+    GP_TRY(dalloc(&c->d_cml[0], na * CML_WORDS));
+    GP_TRY(dalloc(&c->d_cml[1], na * CML_WORDS));
+    GP_TRY(dalloc(&c->d_cmk[0], na));
+    GP_TRY(dalloc(&c->d_cmk[1], na));
+  } else {
+    dfree(&c->d_cml[0]);
+    dfree(&c->d_cml[1]);
+    dfree(&c->d_cmk[0]);
+    dfree(&c->d_cmk[1]);
+  }
   GP_TRY(dalloc(&c->d_amask, (size_t)((c->nnz + 63) / 64 + 2)));
   GP_HIP(hipMemsetAsync(c->d_amask, 0, (size_t)((c->nnz + 63) / 64 + 2) * 8, c->stream));
   GP_TRY(dalloc(&c->d_done_at, na));
@@ -2070,6 +2258,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->early_exit = 1;
   cfg->arc_mask_permille = 0;   // per-arc mask off: its build costs what it saves
   cfg->prefilter_pct = 20;
+  cfg->compact_rows = 0;   // off: the per-receiver loop is latency-bound in the rounds it would serve
   cfg->unfiltered_pct = 90;
   cfg->msg_word_base = 0;
   cfg->flat_max_words = 16;
@@ -2109,7 +2298,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -2134,6 +2323,7 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
   if (cfg->msg_word_base < 0) return set_error(GP_EINVAL, "msg_word_base < 0");
   if (cfg->prefilter_pct < 0) return set_error(GP_EINVAL, "prefilter_pct < 0");
+  if (cfg->compact_rows != 0 && cfg->compact_rows != 1) return set_error(GP_EINVAL, "compact_rows must be 0 or 1");
   if (cfg->arc_mask_permille < 0) return set_error(GP_EINVAL, "arc_mask_permille < 0");
   GP_HIP(hipSetDevice(c->device));
   const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
@@ -2324,6 +2514,8 @@ int gp_reset(gp_ctx* c) {
   c->prev_next_arcs = 0;
   c->prev_new_bits = 0;
   c->prev_receivers = 0;
+  c->cml_written_prev = false;
+  c->cml_read_now = c->cml_write_now = false;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
   GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToDevice, s));
@@ -2417,6 +2609,7 @@ static int round_launch(Ctx* c) {
     ia.ws = c->d_ws;
     ia.fpop = c->d_fpop[c->cur];
     ia.frx = c->d_frx[0] ? c->d_frx[c->cur] : nullptr;
+    ia.cmk = c->d_cmk[0] ? c->d_cmk[c->cur] : nullptr;
     ia.seenpop = c->d_seenpop;
     ia.first = c->cfg.track_first ? c->d_first : nullptr;
     ia.digest = c->cfg.track_digest ? c->d_digest : nullptr;
@@ -2503,7 +2696,8 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->next_arcs = h[S_NEXT_ARCS];
     out->row_bytes = h[S_ROW_BYTES];
     out->mode = c->mode_push ? 1 : 0;
-    out->scan = c->mode_push ? 0 : c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : c->prefilter_now ? 3 : 0;
+    out->scan = c->mode_push ? 0 : (c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : c->prefilter_now ? 3 : 0) |
+                                       (c->cml_read_now ? 4 : 0);
     out->kernel_ms = 0.0;
     if (!c->mode_push && c->nloc() > 0) {
       float kms = 0.f;
@@ -2523,6 +2717,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   c->prev_next_arcs = h[S_NEXT_ARCS];
   c->prev_new_bits = h[S_NEW_BITS];
   c->prev_receivers = h[S_RECEIVERS];
+  c->cml_written_prev = c->cml_write_now;
   c->cur ^= 1;
   c->round = r + 1;
   return 0;

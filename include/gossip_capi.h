@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 9
+#define GP_ABI_VERSION 10
 
 typedef struct gp_ctx gp_ctx;
 
@@ -77,10 +77,11 @@ typedef struct gp_round_stats {
   uint64_t row_bytes;       /* bytes of neighbour rows actually loaded (the pull skips
                                the words a receiver already completed, §3.4)         */
   int32_t mode;             /* 0 = pull expansion, 1 = push expansion                 */
-  int32_t scan;             /* pull arc check: 0 = activity-bitmap probe per arc,
-                               1 = per-arc activity mask built first (§3.2),
-                               2 = none, every in-neighbour row read (§3.4),
-                               3 = probe, low-degree in-lists prefiltered (§3.2)     */
+  int32_t scan;             /* pull arc check (bits 0-1 as a number): 0 = activity-
+                               bitmap probe per arc, 1 = per-arc activity mask built
+                               first, 2 = none, every in-neighbour row read (§3.4),
+                               3 = probe, low-degree in-lists prefiltered (§3.2);
+                               + 4: senders gathered from compact Message-Lists     */
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
@@ -113,6 +114,9 @@ typedef struct gp_config {
   int32_t prefilter_pct;       /* filtered pull rounds with < this % of vertices sending
                                   probe the in-lists of receivers of in-degree <= 16
                                   lane-parallel first (0 = never)       */
+  int32_t compact_rows;        /* 1: 64-word runs keep 128-B compact Message-Lists while
+                                  rows are sparse and gather them instead of full rows
+                                  (single-rank contexts only)           */
   int32_t unfiltered_pct;      /* pull without the per-arc activity check when >= this %
                                   of vertices are senders (0 = never)   */
   int32_t msg_word_base;       /* message shards: this context's message k

@@ -12,6 +12,6 @@ tag, p, v = sys.argv[1:]
 d = json.loads(open(f"gpurun_out/sweep/{tag}.json").read())
 rs = [json.loads(l) for l in open(f"gpurun_out/sweep/{tag}.err") if l.startswith("{")]
 print(p, v, round(d["value"]), "GTEPS", round(d["ms_per_step"], 2), "ms |",
-      " ".join(f"r{r['round']}:{'P' if r['mode'] else 'L'}{r.get('scan', 0)}:{r['expand_ms']:.2f}/{r['kernel_ms']:.2f}" for r in rs))
+      " ".join(f"r{r['round']}:{'P' if r['mode'] else 'L'}{r.get('scan', 0)}:{r['expand_ms']:.2f}/{r['kernel_ms']:.2f}/{r.get('row_bytes', 0)/1e9:.1f}G" for r in rs))
 PY
 done

@@ -36,13 +36,14 @@ MODE_IDS = ["pull", "pull-masked", "pull-unfiltered", "push", "adaptive"]
 
 
 def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096,
-             push_ratio=10.0, unfiltered_pct=90, flat_max_words=16, arc_mask_permille=10, **kw):
+             push_ratio=10.0, unfiltered_pct=90, flat_max_words=16, arc_mask_permille=10, prefilter_pct=20,
+             compact_rows=1, **kw):
     churn = kw.get("churn", False)
     cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(bool(churn or crashes)),
                churn=int(churn), p_fail=kw.get("p_fail", 0.0), churn_seed=kw.get("churn_seed", 0),
                hub_threshold=hub_threshold, push_ratio=push_ratio,
                unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words,
-               arc_mask_permille=arc_mask_permille)
+               arc_mask_permille=arc_mask_permille, prefilter_pct=prefilter_pct, compact_rows=compact_rows)
     eng = _engine(pkg, g, origin, inject, **cfg)
     by_round = {}
     for v, r in crashes:
@@ -66,8 +67,8 @@ def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_th
         for k in STAT_KEYS:
             assert a[k] == b[k], (k, a["round"], a[k], b[k])
     W = eng.words
-    for s in stats:   # word skip only ever drops loads
-        assert s["row_bytes"] <= 8 * W * s["rows_gathered"], s
+    for s in stats:   # word skip and compact records only ever drop loads (+ a record mask each)
+        assert s["row_bytes"] <= (8 * W + (8 if s["scan"] & 4 else 0)) * s["rows_gathered"], s
         if s["mode"] == 1:
             assert s["row_bytes"] == 8 * W * s["rows_gathered"], s
     assert np.array_equal(eng.seen(), ref["seen"][:, :W])
@@ -309,6 +310,33 @@ def test_wide_rows_no_churn(pkg, oracle, mode):
         assert [s["new_bits"] for s in stats] == [s["new_bits"] for s in ref["stats"]]
         assert np.array_equal(eng.digest(), ref["digest"])
     eng.close()
+
+
+@pytest.mark.parametrize("prefilter", [0, 20])
+def test_compact_message_lists(pkg, oracle, prefilter):
+    """W = 64, every message injected at round 0 on a sparse overlay: the early
+    rounds gather senders from compact Message-Lists (scan bit 4), with and
+    without the lane-parallel prefilter; results are those of the oracle and of
+    a run with compact rows off."""
+    rp, col = oracle.chung_lu(200_000, 8, 2.5, 31)
+    g = pkg.CSR(200_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 4096, seed=31)
+    r = _compare(pkg, oracle, g, origin, first=False, push_ratio=0.0, prefilter_pct=prefilter, arc_mask_permille=0,
+                 compact_rows=1)
+    assert any(s["scan"] & 4 for s in r["stats"])
+    assert any((s["scan"] & 3) == (3 if prefilter else 0) and s["scan"] & 4 for s in r["stats"])
+    r["eng"].close()
+    with pkg.GossipEngine(0, track_digest=1, push_ratio=0.0, prefilter_pct=prefilter, compact_rows=0,
+                          arc_mask_permille=0, unfiltered_pct=90, flat_max_words=16, hub_threshold=4096) as eng:
+        eng.load_graph(g)
+        eng.set_messages(origin)
+        eng.reset()
+        stats = eng.run()
+        assert not any(s["scan"] & 4 for s in stats)
+        for a, b in zip(stats, r["stats"]):
+            for k in STAT_KEYS + ("rows_gathered", "arcs_scanned", "rows_written"):
+                assert a[k] == b[k], k
+        assert np.array_equal(eng.digest(), r["ref"]["digest"])
 
 
 @pytest.mark.parametrize("shards", [2, 4])
