@@ -230,7 +230,7 @@ constexpr u64 CML_DENSE = ~0ull;
 #define GP_EXPAND_WAVES 0
 #endif
 #if GP_EXPAND_WAVES > 0
-#define EXPAND_BOUNDS __launch_bounds__(BLOCK, GP_EXPAND_WAVES)
+#define EXPAND_BOUNDS __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GP_EXPAND_WAVES)))
 #else
 #define EXPAND_BOUNDS __launch_bounds__(BLOCK)
 #endif
@@ -239,21 +239,26 @@ constexpr u64 CML_DENSE = ~0ull;
 #define GP_ROWS_IN_FLIGHT 4
 #endif
 
-// per-wave LDS of the pull kernels
-struct WaveLds {
+// per-wave LDS of the pull kernels; the mode-specific arrays take one element
+// when their mode is compiled out (LDS is what bounds the waves per CU)
+constexpr int PRE_IDS = 8;       // active neighbours kept per prefiltered vertex
+constexpr int PRE_MAX_DEG = 16;  // in-degree up to which the lane phase probes
+template <bool PRE, bool CML>
+struct WaveLdsT {
+  static constexpr bool kPre = PRE, kCml = CML;
   u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
   int32_t idx[64];      // active neighbours of one pass
   uint32_t tot[64];     // k_expand: new bits of the wave's vertex k (committed after the loop)
   u64 dig[64];          // k_expand: digest terms of vertex k
   int64_t rp[65];       // k_expand: row_ptr of the wave's vertices (rp[k], rp[k + 1])
   int32_t mi[64];       // k_expand: component-mask row of vertex k (early-exit rounds)
-  u64 msk[64];          // compact-row rounds: the staged senders' record masks
-  u64 cm[64];           // compact-row rounds: mask word of the wave's vertex k (committed)
-  int32_t pre[64][8];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
-  uint8_t np[64];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
+  u64 msk[CML ? 64 : 1];          // compact-row rounds: the staged senders' record masks
+  u64 cm[CML ? 64 : 1];           // compact-row rounds: mask word of the wave's vertex k (committed)
+  int32_t pre[PRE ? 64 : 1][PRE_IDS];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
+  uint8_t np[PRE ? 64 : 1];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
 };
-constexpr int PRE_IDS = 8;       // active neighbours kept per prefiltered vertex
-constexpr int PRE_MAX_DEG = 16;  // in-degree up to which the lane phase probes
+using WaveLds = WaveLdsT<false, false>;
+#define LDS_OF(MODE) WaveLdsT<((MODE) & 3) == SCAN_PRE, ((MODE) & SCAN_CML) != 0>
 
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -399,8 +404,8 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* 
 
 // compact-row rounds: the staged senders' record masks into L.msk (one
 // instruction for the pass), and the record/row bytes they stand for
-template <int W>
-__device__ __forceinline__ void stage_masks(const ExpandArgs& a, WaveLds& L, const int32_t* idx, int cnt,
+template <int W, class LDS>
+__device__ __forceinline__ void stage_masks(const ExpandArgs& a, LDS& L, const int32_t* idx, int cnt,
                                             WaveStats& st) {
   const int lane = threadIdx.x & 63;
   u64 bytes = 0;
@@ -416,8 +421,8 @@ __device__ __forceinline__ void stage_masks(const ExpandArgs& a, WaveLds& L, con
 // gather_rows over compact records (no early exit: sparse rounds only).  Lane
 // (g, lw) holds words 2lw, 2lw + 1: from a compact record it loads the packed
 // entries of those words if they are nonzero, from a dense sender its piece.
-template <int W>
-__device__ __forceinline__ void gather_rows_cml(const ExpandArgs& a, const WaveLds& L, const int32_t* idx, int cnt,
+template <int W, class LDS>
+__device__ __forceinline__ void gather_rows_cml(const ExpandArgs& a, const LDS& L, const int32_t* idx, int cnt,
                                                 int g, int lw, u64x2& acc, WaveStats& st) {
   constexpr int RPI = Geo<W>::RPI;
   static_assert(W == 64, "compact records hold 64-word rows");
@@ -450,7 +455,8 @@ __device__ __forceinline__ void gather_rows_cml(const ExpandArgs& a, const WaveL
 
 // stage one pass of probed neighbours (e: this lane's entry, -1 = none) in
 // LDS; returns their count
-__device__ __forceinline__ int stage_pass(WaveLds& L, int32_t e) {
+template <class LDS>
+__device__ __forceinline__ int stage_pass(LDS& L, int32_t e) {
   const u64 m = __ballot(e >= 0);
   if (e >= 0) L.idx[lane_rank(m)] = e;
   wave_sync_lds();
@@ -465,8 +471,8 @@ __device__ __forceinline__ u64x2 load_seen(const ExpandArgs& a, int v, uint32_t 
 
 // early exit: park the receiver's seen row in LDS (finish_row reuses it) and
 // return, in group-0 lanes, the messages of its component it still lacks
-template <int W>
-__device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, WaveLds& L, int g, int lw,
+template <int W, class LDS>
+__device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, LDS& L, int g, int lw,
                                                    uint32_t sv_slot, int32_t mrow) {
   constexpr int WPL = Geo<W>::WPL;
   // every row slot group loads the same pieces (one fetch per line): each lane
@@ -482,8 +488,8 @@ __device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, W
 
 // per-receiver scan of arcs [b, e): 64 arcs per pass -- column ids, activity
 // probes, staging, gather
-template <int W, int MODE>
-__device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int64_t e, WaveLds& L, int lane,
+template <int W, int MODE, class LDS>
+__device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int64_t e, LDS& L, int lane,
                                             int g, int lw, u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
   for (int64_t j0 = b; j0 < e; j0 += 64) {
     const int n = (int)min((int64_t)64, e - j0);
@@ -585,9 +591,9 @@ __device__ __forceinline__ u64 write_cml(u64* __restrict__ cml, int v, int g, in
 // go to L.tot/L.dig[k] and the wave commits them for its 64 vertices at once,
 // coalesced, after its loop -- one scattered read-modify-write chain less per
 // receiver, and whole cache lines instead of 1-8 byte pieces.
-template <int W, bool DEFER = false, bool CMLW = true>
+template <int W, bool DEFER = false, bool CMLW = true, class LDS = WaveLds>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
-                                           int g, int lw, WaveStats& st, WaveLds& L, bool have_sv,
+                                           int g, int lw, WaveStats& st, LDS& L, bool have_sv,
                                            uint32_t sv_slot, int k = 0) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
@@ -638,16 +644,16 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
       if (WPL == 2 && nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + lw * WPL + 1), nw.y);
     }
     t = wave_xor_u64(t);
-    if (DEFER) {
+    if constexpr (DEFER) {
       if (lane == 0) L.dig[k] = t;
     } else if (lane == 0) {
       a.digest[i] ^= t;
     }
   }
-  if (DEFER) {
+  if constexpr (DEFER) {
     if (lane == 0) {
       L.tot[k] = tot;
-      if (CMLW) L.cm[k] = cm;
+      if constexpr (CMLW && LDS::kCml) L.cm[k] = cm;
     }
   } else {
     if (lane == 0) {
@@ -666,7 +672,8 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
 
 // k_expand's commit of the deferred per-vertex words: lane k holds vertex
 // base + k (need: it was scanned)
-__device__ __forceinline__ void commit_vertices(const ExpandArgs& a, WaveLds& L, int64_t li, bool need,
+template <class LDS>
+__device__ __forceinline__ void commit_vertices(const ExpandArgs& a, LDS& L, int64_t li, bool need,
                                                 WaveStats& st) {
   wave_sync_lds();
   const int lane = threadIdx.x & 63;
@@ -675,7 +682,8 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, WaveLds& L,
     const int v = (int)(a.vbegin + li);
     const uint32_t tot = L.tot[lane];
     a.fpop_next[v] = tot;
-    if (a.cmk_next) a.cmk_next[v] = tot ? L.cm[lane] : 0ull;
+    if constexpr (LDS::kCml)
+      if (a.cmk_next) a.cmk_next[v] = tot ? L.cm[lane] : 0ull;
     if (tot) {
       a.seenpop[li] += tot;
       a.sp[v] = (uint8_t)a.wslot;
@@ -695,11 +703,11 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, WaveLds& L,
 template <int W, int MODE>
 __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
-  __shared__ WaveLds s_w[WAVES];
+  __shared__ LDS_OF(MODE) s_w[WAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
-  WaveLds& L = s_w[wib];
+  auto& L = s_w[wib];
   WaveStats st;
   ws_zero(st);
   const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
