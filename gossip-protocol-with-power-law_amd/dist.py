@@ -17,6 +17,7 @@ RCCL unique id to every rank, aligns the timed region and gathers per-rank
 results for checking.
 """
 import os
+import sys
 
 import numpy as np
 
@@ -44,10 +45,22 @@ def partition_bounds(n, nranks):
 
 
 def init(backend="gloo"):
+    """Control-plane process group.  Gloo's C++ side prints its peer-connection
+    messages to stdout, where rank 0's one JSON line (bench.py) must stand
+    alone: stdout is pointed at stderr while the group connects."""
     import torch.distributed as dist
     world, rank, _ = env()
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group(backend, rank=rank, world_size=world)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     return dist if world > 1 else None
 
 

@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_LDS"
 P2="SQ_INSTS_SALU SQ_INSTS_SMEM SQ_LEVEL_WAVES SQ_WAVES SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
-for tree in . _old; do
+for tree in ${TREES:-. _old}; do
   out=$GRAFT_REPO_ROOT/gpurun_out/sq/$(echo $tree | tr -d './')x
   mkdir -p $out
   i=0
