@@ -32,11 +32,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--log2n", type=int, default=24)
+    ap.add_argument("--workload", choices=("c4", "c5"), default="c4",
+                    help="c4: BASELINE config 4 (2^24 x 4096, the headline line); c5: config 5, "
+                         "2^26 nodes with 1%%/round crashes, 3-miss detection and seed removal")
+    ap.add_argument("--log2n", type=int, default=None)
     ap.add_argument("--dbar", type=float, default=16.0)
     ap.add_argument("--gamma", type=float, default=2.5)
     ap.add_argument("--messages", type=int, default=4096)
-    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--p-fail", type=float, default=0.01, help="c5: per-round crash probability")
     ap.add_argument("--hub-threshold", type=int, default=4096)
     ap.add_argument("--push-ratio", type=float, default=400.0)
     ap.add_argument("--early-exit", type=int, default=1)
@@ -58,7 +62,13 @@ def parse():
                          "partition with an RCCL all-gather of the next rows every round")
     ap.add_argument("--profile-steps", action="store_true",
                     help="print per-round stats of the last step to stderr")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c5 = a.workload == "c5"
+    if a.log2n is None:
+        a.log2n = 26 if c5 else 24
+    if a.seed is None:
+        a.seed = 5 if c5 else 4
+    return a
 
 
 def round_bytes(st, words, nloc):
@@ -115,12 +125,14 @@ def cpu_baseline(args, eng, origin, pkg):
     threads = args.cpu_threads or min(os.cpu_count() or 1, 16)
     o = origin[:args.cpu_messages]
     t0 = time.perf_counter()
-    ref = oracle_lib.run(g, o, nthreads=threads, want_forwards=False)
+    churn = args.workload == "c5"
+    ref = oracle_lib.run(g, o, nthreads=threads, want_forwards=False, churn=churn,
+                         p_fail=args.p_fail if churn else 0.0, churn_seed=args.seed)
     dt = time.perf_counter() - t0
     sends = sum(s["sends"] for s in ref["stats"])
     return {"value": sends / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
             "sample": f"oracle/gossip_oracle.c, same 2^{args.log2n}-node overlay, first "
-                      f"{len(o)} of {args.messages} messages, full run ({ref['rounds']} rounds, "
+                      f"{len(o)} of {args.messages} messages, full run{' with churn' if churn else ''} ({ref['rounds']} rounds, "
                       f"{sends} edge-deliveries, {dt:.1f} s, {threads} OpenMP threads)"}
 
 
@@ -140,6 +152,9 @@ def main():
                            unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words,
                            arc_mask_permille=args.arc_mask_permille, compact_rows=args.compact_rows,
                            prefilter_pct=args.prefilter_pct)
+    churn = args.workload == "c5"
+    if churn:   # Bernoulli crashes of live vertices, stream seeded by the run seed
+        eng.configure(churn=1, p_fail=args.p_fail, churn_seed=args.seed, miss_threshold=3)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()
@@ -195,14 +210,14 @@ def main():
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
                                                 "rows_written", "row_bytes", "atomics",
-                                                "scan", "expand_ms", "kernel_ms", "exchange_ms")}),
+                                                "crashed", "reports", "removals", "scan", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, eng, origin, pkg)
     if rank == 0:
         out = {
-            "metric": "gossip edge-deliveries/s (GTEPS) & HBM roofline %, 2^24 nodes x 4096 msgs",
+            "metric": f"gossip edge-deliveries/s (GTEPS) & HBM roofline %, 2^{args.log2n} nodes x {args.messages} msgs",
             "value": sends / dt / 1e9,
             "unit": "GTEPS",
             "n_gpus": world,
@@ -214,7 +229,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (device-built Chung-Lu overlay, seeded origins)",
-            "config": {"workload": "C4: Chung-Lu gamma=2.5 overlay, full forward-once gossip run",
+            "config": {"workload": ("C5: Chung-Lu gamma=2.5 overlay with churn (p_fail per round, 3-miss "
+                                    "liveness, seed removal), full forward-once gossip run" if churn else
+                                    "C4: Chung-Lu gamma=2.5 overlay, full forward-once gossip run"),
                        "n": n, "arcs": nnz, "mean_degree": nnz / n, "messages": args.messages,
                        "words_per_row": eng.words, "rounds_per_step": rounds / args.steps,
                        "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,

@@ -1538,6 +1538,35 @@ __global__ void k_done_at(const int32_t* __restrict__ comp, const uint32_t* __re
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (v < n) done_at[v] = cnt[comp[v]];
 }
+// Lost messages (origin down at the inject round, S_LOST) never enter any
+// Message-List: drop them from the component targets of this run, so that the
+// early-exit and done-skip tests of E_r still fire for the component's
+// vertices.  One thread per (group, word) of this round's injection span; the
+// state test is k_inject's own (no kernel between them changes state).
+__global__ void k_lost_clear(const int32_t* __restrict__ origin, const u64* __restrict__ bits,
+                             const uint32_t* __restrict__ cnt, const uint8_t* __restrict__ state,
+                             const int32_t* __restrict__ midx, u64* __restrict__ cmask,
+                             uint32_t* __restrict__ lostcnt, int64_t off, int64_t groups, int32_t words) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= groups * words) return;
+  const int64_t gi = off + t / words;
+  const int32_t w = (int32_t)(t % words);
+  const int32_t o = origin[gi];
+  if (!(state[o] & ST_DOWN)) return;
+  const int32_t k = midx[o];
+  atomicAnd(cmask + (size_t)k * words + w, ~bits[gi * words + w]);
+  if (w == 0) atomicAdd(lostcnt + k, cnt[gi]);
+}
+__global__ void k_done_fix(const int32_t* __restrict__ midx, const uint32_t* __restrict__ lostcnt,
+                           uint32_t* __restrict__ done_at, int64_t n) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  const int32_t k = midx[v];
+  if (k >= 0) {
+    const uint32_t l = lostcnt[k];
+    if (l) done_at[v] -= l;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // injection (I_r): one wave per (round, origin) group.  The origin's seen row
@@ -1957,7 +1986,13 @@ static int launch_expand(Ctx* c) {
   // direction: push when the senders' arcs are a small share of all arcs
   const int r = c->round;
   // early exit pays once frontier rows are dense: >= m/16 new bits per vertex last round
-  c->early_exit_now = c->cfg.early_exit != 0 && (double)c->prev_new_bits * 16.0 >= (double)c->n * (double)c->m;
+  // or once most messages are held: receivers then miss a few words at most, and
+  // the word skip loads only those (under churn the component targets may be
+  // out of reach -- a message cut off by crashes -- so the done-skip alone
+  // leaves nearly every receiver scanning whole rows)
+  c->early_exit_now = c->cfg.early_exit != 0 &&
+                      ((double)c->prev_new_bits * 16.0 >= (double)c->n * (double)c->m ||
+                       (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m);
   const u64 inj = (size_t)r < c->inj_arcs.size() ? (u64)c->inj_arcs[(size_t)r] : 0ull;
   const double est = (double)((r == 0 ? 0ull : c->prev_next_arcs) + inj);
   c->mode_push = c->cfg.push_ratio > 0.0 && est * c->cfg.push_ratio <= (double)c->nnz;
@@ -2084,6 +2119,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
@@ -2223,6 +2259,14 @@ static int compute_done_at(Ctx* c, int64_t groups) {
   GP_HIP(hipMemsetAsync(c->d_midx, 0xFF, (size_t)c->n_alloc * 4, s));
   hipLaunchKernelGGL(k_midx, dim3(grid_for(c->n, 256)), dim3(256), 0, s, c->d_comp, ior, c->d_midx, c->n);
   GP_HIP(hipGetLastError());
+  // pristine targets (a run drops its lost messages from the working ones)
+  c->cmask_rows = (int32_t)(masks.size() / W);
+  GP_TRY(dalloc(&c->d_cmask0, masks.size()));
+  GP_TRY(dalloc(&c->d_done_at0, (size_t)c->n_alloc));
+  GP_TRY(dalloc(&c->d_lostcnt, (size_t)c->cmask_rows));
+  GP_HIP(hipMemcpyAsync(c->d_cmask0, c->d_cmask, masks.size() * 8, hipMemcpyDeviceToDevice, s));
+  GP_HIP(hipMemcpyAsync(c->d_done_at0, c->d_done_at, (size_t)c->n_alloc * 4, hipMemcpyDeviceToDevice, s));
+  c->done_dirty = false;
   GP_HIP(hipStreamSynchronize(s));
   dfree(&ior);
   return 0;
@@ -2307,6 +2351,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
   dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -2506,6 +2551,12 @@ int gp_reset(gp_ctx* c) {
   if (!c->done_at_valid) {
     GP_TRY(compute_done_at(c, c->n_groups));
     c->done_at_valid = true;
+  } else if (c->done_dirty) {   // undo the previous run's lost-message drops
+    GP_HIP(hipMemcpyAsync(c->d_cmask, c->d_cmask0, (size_t)c->cmask_rows * c->words * 8,
+                          hipMemcpyDeviceToDevice, c->stream));
+    GP_HIP(hipMemcpyAsync(c->d_done_at, c->d_done_at0, (size_t)c->n_alloc * 4, hipMemcpyDeviceToDevice,
+                          c->stream));
+    c->done_dirty = false;
   }
   const size_t W = (size_t)c->words, na = (size_t)c->n_alloc, nl = (size_t)std::max<int64_t>(c->nloc(), 1);
   hipStream_t s = c->stream;
@@ -2522,6 +2573,7 @@ int gp_reset(gp_ctx* c) {
   c->prev_next_arcs = 0;
   c->prev_new_bits = 0;
   c->prev_receivers = 0;
+  c->held_bits = 0;
   c->cml_written_prev = false;
   c->cml_read_now = c->cml_write_now = false;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
@@ -2632,6 +2684,16 @@ static int round_launch(Ctx* c) {
     ia.r = r;
     hipLaunchKernelGGL(k_inject, dim3(grid_for(ia.groups, WAVES)), dim3(BLOCK), 0, s, ia);
     GP_HIP(hipGetLastError());
+    if (c->liveness_active && c->cmask_rows > 0) {   // origins may be down: drop lost messages
+      GP_HIP(hipMemsetAsync(c->d_lostcnt, 0, (size_t)c->cmask_rows * 4, s));
+      hipLaunchKernelGGL(k_lost_clear, dim3(grid_for(ia.groups * c->words, 256)), dim3(256), 0, s,
+                         c->d_inj_origin, c->d_inj_bits, c->d_inj_cnt, c->d_state, c->d_midx, c->d_cmask,
+                         c->d_lostcnt, ia.off, ia.groups, c->words);
+      hipLaunchKernelGGL(k_done_fix, dim3(grid_for(c->n, 256)), dim3(256), 0, s, c->d_midx, c->d_lostcnt,
+                         c->d_done_at, c->n);
+      GP_HIP(hipGetLastError());
+      c->done_dirty = true;
+    }
   }
 
   if (c->cfg.track_msg_forwards) {   // sends of round r per message (owned senders)
@@ -2725,6 +2787,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   c->prev_next_arcs = h[S_NEXT_ARCS];
   c->prev_new_bits = h[S_NEW_BITS];
   c->prev_receivers = h[S_RECEIVERS];
+  c->held_bits += h[S_INJECTED] + h[S_NEW_BITS];
   c->cml_written_prev = c->cml_write_now;
   c->cur ^= 1;
   c->round = r + 1;
@@ -2781,10 +2844,12 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     }
   }
   gp_round_stats sum;
+  std::vector<u64> own_held((size_t)nctx, 0);
   std::memset(&sum, 0, sizeof(sum));
   for (int32_t k = 0; k < nctx; ++k) {
     gp_round_stats st;
     GP_TRY(round_collect(ctxs[k], &st));
+    own_held[(size_t)k] = st.injected + st.new_bits;
     sum.round = st.round;
     sum.overflow |= st.overflow;
     sum.injected += st.injected; sum.lost += st.lost; sum.new_bits += st.new_bits;
@@ -2803,6 +2868,8 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     ctxs[k]->prev_next_arcs = sum.next_arcs;
     ctxs[k]->prev_new_bits = sum.new_bits;
     ctxs[k]->prev_receivers = sum.receivers;
+    // round_collect added the context's own share; every context holds the sum
+    ctxs[k]->held_bits += sum.injected + sum.new_bits - own_held[(size_t)k];
   }
   if (out) *out = sum;
   return 0;

@@ -99,6 +99,7 @@ struct Ctx {
   bool early_exit_now = false;      // coverage-checked scan this round
   u64 prev_new_bits = 0;            // new bits of the last round (global)
   u64 prev_receivers = 0;           // receivers of the last round (global)
+  u64 held_bits = 0;                // messages held so far, summed over vertices (global)
   bool unfiltered_now = false;      // this round's pull skips the activity check
   bool arc_mask_now = false;        // this round's filtered pull reads the per-arc mask
   bool prefilter_now = false;       // this round's filtered pull probes low-degree in-lists lane-parallel
@@ -116,7 +117,15 @@ struct Ctx {
   std::vector<int32_t> h_inj_origin;   // host copies of the injection groups
   std::vector<u64> h_inj_bits;
   std::vector<int32_t> h_deg_out;
-  uint32_t* d_done_at = nullptr;    // [n_alloc] messages of the vertex's component
+  uint32_t* d_done_at = nullptr;    // [n_alloc] messages of the vertex's component (this run)
+  // pristine copies of done_at / cmask: a message whose origin is down at its
+  // inject round never exists, so the run drops it from its component's target
+  // (k_lost_clear, k_done_fix); gp_reset restores the pristine targets
+  uint32_t* d_done_at0 = nullptr;   // [n_alloc]
+  u64* d_cmask0 = nullptr;          // [K][W]
+  uint32_t* d_lostcnt = nullptr;    // [K] messages lost per component this round
+  int32_t cmask_rows = 0;           // K
+  bool done_dirty = false;          // the working targets differ from the pristine ones
   u64* d_msg_cov = nullptr;    // [W*64]
   u64* d_msg_fwd = nullptr;    // [W*64]
   gp_report* d_reports = nullptr;

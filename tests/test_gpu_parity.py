@@ -289,6 +289,40 @@ def test_wide_rows_churn(pkg, oracle, mode):
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
+def test_lost_messages_drop_from_targets(pkg, oracle, mode):
+    """Messages whose origin is down at the inject round are dropped from the
+    early-exit targets of their component for that run (k_lost_clear,
+    k_done_fix): the run stays bit-exact, and gp_reset restores the targets, so
+    repeated runs on one context are identical."""
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
+    rp, col = oracle.chung_lu(40_000, 10, 2.4, 23)
+    g = pkg.CSR(40_000, rp, col, False)
+    m = 4096
+    origin = pkg.overlay.random_origins(g.n, m, seed=23)
+    inject = (np.arange(m) % 5).astype(np.int32)
+    crashes = [(int(v), int(r)) for v, r in zip(origin[:300], inject[:300])]   # down when injected
+    r = _compare(pkg, oracle, g, origin, inject, crashes=crashes, first=False, push_ratio=push_ratio,
+                 unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask,
+                 churn=True, p_fail=0.02, churn_seed=9)
+    assert sum(s["lost"] for s in r["stats"]) >= 300
+    eng, ref = r["eng"], r["ref"]
+    by_round = {}
+    for v, rr in crashes:
+        by_round.setdefault(rr, []).append(v)
+    for _ in range(2):
+        eng.reset()
+        stats = []
+        for rr in range(len(ref["stats"])):
+            if rr in by_round:
+                eng.crash(by_round[rr])
+            stats.append(eng.round())
+        assert [s["new_bits"] for s in stats] == [s["new_bits"] for s in ref["stats"]]
+        assert [s["lost"] for s in stats] == [s["lost"] for s in ref["stats"]]
+        assert np.array_equal(eng.digest(), ref["digest"])
+    eng.close()
+
+
+@pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_wide_rows_no_churn(pkg, oracle, mode):
     """W = 64 without liveness: unfiltered dense rounds read whole Message-List
     rows of every in-neighbour (stale slots zeroed by k_fixup_rows); repeated
