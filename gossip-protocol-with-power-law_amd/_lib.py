@@ -115,9 +115,12 @@ SIGNATURES = {
     "gp_reports": (ctypes.c_int, [_P, ctypes.POINTER(Report), _I64, _PI64]),
     "gp_synchronize": (ctypes.c_int, [_P]),
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
+    "gp_checkpoint_size": (ctypes.c_int, [_P, _PI64]),
+    "gp_checkpoint_save": (ctypes.c_int, [_P, _P, _I64]),
+    "gp_checkpoint_load": (ctypes.c_int, [_P, _P, _I64]),
 }
 
-ABI_VERSION = 10   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 11   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

@@ -2280,7 +2280,6 @@ using namespace gp;
 // C-ABI
 extern "C" {
 
-struct gp_ctx : public gp::Ctx {};
 
 int gp_abi_version(void) { return GP_ABI_VERSION; }
 const char* gp_last_error(void) { return g_err.c_str(); }

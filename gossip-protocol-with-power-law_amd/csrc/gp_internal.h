@@ -203,3 +203,6 @@ int build_gather_order(Ctx* c);
 int finish_graph(Ctx* c);
 
 }  // namespace gp
+
+// the ABI handle is the context itself
+struct gp_ctx : public gp::Ctx {};

@@ -168,6 +168,33 @@ class GossipEngine:
     def synchronize(self):
         check(self._lib.gp_synchronize(self._ctx))
 
+    # -- checkpoints ----------------------------------
+    def checkpoint(self):
+        """The context's whole per-run state between rounds, as an opaque
+        uint8 blob (gp_checkpoint_save)."""
+        nb = ctypes.c_int64()
+        check(self._lib.gp_checkpoint_size(self._ctx, ctypes.byref(nb)))
+        blob = np.empty(nb.value, dtype=np.uint8)
+        check(self._lib.gp_checkpoint_save(self._ctx, _ptr(blob), blob.nbytes))
+        return blob
+
+    def restore(self, blob):
+        """Continue the run a checkpoint() blob captured: same overlay,
+        messages, partition and tracked outputs (gp_checkpoint_load)."""
+        b = np.ascontiguousarray(blob, dtype=np.uint8)
+        check(self._lib.gp_checkpoint_load(self._ctx, _ptr(b), b.nbytes))
+
+    def save_checkpoint(self, path):
+        """Write checkpoint() to an .npz (uncompressed: Message-List rows are
+        the bulk and do not compress well once dense)."""
+        np.savez(path, state=self.checkpoint(), n=self.n, m=self.m, words=self.words)
+
+    def load_checkpoint(self, path):
+        with np.load(path, allow_pickle=False) as z:
+            if int(z["n"]) != self.n or int(z["m"]) != self.m:
+                raise ValueError(f"{path}: checkpoint of n={int(z['n'])}, m={int(z['m'])}")
+            self.restore(z["state"])
+
     # -- outputs -----------------------------------------------------------
     def _read(self, what, arr):
         check(self._lib.gp_read(self._ctx, what, _ptr(arr), arr.nbytes))

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 10
+#define GP_ABI_VERSION 11
 
 typedef struct gp_ctx gp_ctx;
 
@@ -195,6 +195,18 @@ int gp_read(gp_ctx* ctx, int32_t what, void* host, int64_t bytes);
 int gp_reports(gp_ctx* ctx, gp_report* buf, int64_t cap, int64_t* n_out);
 int gp_synchronize(gp_ctx* ctx);
 int gp_info(gp_ctx* ctx, int64_t* n, int64_t* nnz, int32_t* m, int32_t* words);
+
+/* Checkpoints (no reference counterpart -- the
+ * reference's peers keep no state across restarts).  Taken between rounds:
+ * the blob holds the whole per-run state of this context (Message-List rows in
+ * canonical form, popcounts, liveness state, counters, tracked outputs, round
+ * number and direction history).  Loading it into a context with the same
+ * overlay, messages, partition and tracked outputs continues the run exactly
+ * as if it had never stopped.  The blob is opaque; gp_checkpoint_size gives
+ * its length (8*W bytes per vertex plus ~30 B of vertex state). */
+int gp_checkpoint_size(gp_ctx* ctx, int64_t* bytes);
+int gp_checkpoint_save(gp_ctx* ctx, void* host, int64_t bytes);
+int gp_checkpoint_load(gp_ctx* ctx, const void* host, int64_t bytes);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,7 @@
+# checkpoint/restore parity tests
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -m gpu -k "checkpoint" > gpurun_out/pytest_ckpt.log 2>&1
+rc=$?; echo "pytest exit $rc"; tail -30 gpurun_out/pytest_ckpt.log
+exit $rc

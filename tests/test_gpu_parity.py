@@ -323,6 +323,65 @@ def test_lost_messages_drop_from_targets(pkg, oracle, mode):
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
+@pytest.mark.parametrize("stop,p_fail", [(1, 0.01), (3, 0.01), (2, 0.0), (4, 0.0)])
+def test_checkpoint_restore_continues_exactly(pkg, oracle, mode, stop, p_fail, tmp_path):
+    """gp_checkpoint_save after `stop` rounds, then (a) the same context runs
+    on, (b) a fresh context loads the .npz and runs on, (c) the first context
+    loads it again after finishing and re-runs the tail: all three match the
+    oracle's uninterrupted run bit for bit (counters, Message-Lists, first
+    receipts, digests, per-message coverage/forwards, dead-node reports)."""
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
+    rp, col = oracle.chung_lu(30_000, 10, 2.4, 31)
+    g = pkg.CSR(30_000, rp, col, False)
+    m = 4096
+    origin = pkg.overlay.random_origins(g.n, m, seed=31)
+    inject = (np.arange(m) % 5).astype(np.int32)
+    kw = dict(churn=p_fail > 0, p_fail=p_fail, churn_seed=13)
+    cfg = dict(track_first=1, track_digest=1, track_msg_forwards=1, churn=int(p_fail > 0), p_fail=p_fail,
+               churn_seed=13, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct,
+               flat_max_words=flat_max_words, arc_mask_permille=arc_mask, compact_rows=1)
+    ref = oracle.run(g, origin, inject, want_first=True, **kw)
+
+    def tail(eng):
+        stats, reports = [], []
+        while True:
+            st = eng.round()
+            stats.append(st)
+            rep, _ = eng.reports()
+            reports.extend(map(tuple, rep.tolist()))
+            if st["new_bits"] == 0 and st["round"] >= 4:
+                return stats, reports
+
+    def check(eng, stats, reports):
+        assert len(stats) == ref["rounds"] - stop
+        for a, b in zip(stats, ref["stats"][stop:]):
+            for k in STAT_KEYS:
+                assert a[k] == b[k], (k, a["round"], a[k], b[k])
+        eng.finalize()
+        assert np.array_equal(eng.seen(), ref["seen"][:, :eng.words])
+        assert np.array_equal(eng.first(), ref["first"])
+        assert np.array_equal(eng.digest(), ref["digest"])
+        assert np.array_equal(eng.coverage(), ref["coverage"])
+        assert np.array_equal(eng.forwards(), ref["forwards"])
+        ref_tail = [tuple(x) for x in ref["reports"].tolist() if x[2] >= stop]
+        assert sorted(reports) == sorted(ref_tail)
+
+    a = _engine(pkg, g, origin, inject, **cfg)
+    for _ in range(stop):
+        a.round()
+    path = tmp_path / "ck.npz"
+    a.save_checkpoint(path)
+    check(a, *tail(a))
+    b = _engine(pkg, g, origin, inject, **cfg)
+    b.load_checkpoint(path)
+    check(b, *tail(b))
+    b.close()
+    a.load_checkpoint(path)
+    check(a, *tail(a))
+    a.close()
+
+
+@pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_wide_rows_no_churn(pkg, oracle, mode):
     """W = 64 without liveness: unfiltered dense rounds read whole Message-List
     rows of every in-neighbour (stale slots zeroed by k_fixup_rows); repeated
