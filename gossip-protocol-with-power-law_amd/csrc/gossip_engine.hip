@@ -828,10 +828,18 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
 // receiver side then runs lane-parallel, one receiver per lane.  No early exit
 // (narrow rows are cheap next to the arc scan).
 constexpr int FLAT_CAP = 512;   // arc positions per owner window
-// row wave-instructions in flight per lane (VGPRs vs occupancy: 2 -> 66 VGPRs at W = 8)
-#ifndef GP_FLAT_ROWS_IN_FLIGHT
-#define GP_FLAT_ROWS_IN_FLIGHT 2
+// row wave-instructions in flight per lane (VGPRs vs occupancy: 2 -> 66 VGPRs
+// at W = 8).  Measured on the message shards (same box A/B): W = 8 (64-B rows,
+// 16 per instruction) 15.6 -> 15.2 ms with 3 for a 512-message shard; W = 16
+// 28.3 -> 24.4 ms with 4 and 22.9 ms with 6 for a 1024-message shard (8: 25.6)
+#ifndef GP_FLAT_RIF_NARROW
+#define GP_FLAT_RIF_NARROW 3
 #endif
+#ifndef GP_FLAT_RIF_WIDE
+#define GP_FLAT_RIF_WIDE 6
+#endif
+template <int W>
+struct FlatRIF { static constexpr int value = W >= 16 ? GP_FLAT_RIF_WIDE : GP_FLAT_RIF_NARROW; };
 // receivers per wave: 64, or 32 at W = 32 so that the LDS accumulators (8 KB
 // per wave) leave room for 4 blocks per CU
 template <int W>
@@ -857,6 +865,7 @@ __device__ __forceinline__ u64 flat_pass(const ExpandArgs& a, FlatLds<W>& F, int
   constexpr int RPI = Geo<W>::RPI;
   constexpr int WPL = Geo<W>::WPL;
   constexpr int QA = 4;
+  constexpr int RIF = FlatRIF<W>::value;
   const uint32_t excl = wave_excl_scan_u32(sdeg, lane);
   const uint32_t incl = excl + sdeg;
   const uint32_t T = (uint32_t)__shfl((int)incl, 63);
@@ -936,16 +945,16 @@ __device__ __forceinline__ u64 flat_pass(const ExpandArgs& a, FlatLds<W>& F, int
         }
         wave_sync_lds();
         gathered += (u64)cnt;
-        for (int k0 = 0; k0 < cnt; k0 += GP_FLAT_ROWS_IN_FLIGHT * RPI) {
-          u64x2 r[GP_FLAT_ROWS_IN_FLIGHT];
+        for (int k0 = 0; k0 < cnt; k0 += RIF * RPI) {
+          u64x2 r[RIF];
 #pragma unroll
-          for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
+          for (int t = 0; t < RIF; ++t) {
             const int k = k0 + g + t * RPI;
             r[t] = u64x2{0, 0};
             if (k < cnt) r[t] = load_piece<W>(a.rows, F.idx[k], lw);
           }
 #pragma unroll
-          for (int t = 0; t < GP_FLAT_ROWS_IN_FLIGHT; ++t) {
+          for (int t = 0; t < RIF; ++t) {
             const int k = k0 + g + t * RPI;
             if (k < cnt) {
               u64* dst = &F.acc[F.vtx[k]][lw * WPL];

@@ -9,7 +9,8 @@ mkdir -p $OUT
 F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 $2"
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/gossip_engine.hip -o $OUT/ge.o &
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/graph_build.hip -o $OUT/gb.o &
+/opt/rocm/bin/hipcc $F -c $PKG/csrc/checkpoint.hip -o $OUT/ck.o &
 wait
-/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o -o $PKG/_variants/$1.so -lrccl
+/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o $OUT/ck.o -o $PKG/_variants/$1.so -lrccl
 rm -rf $OUT
 echo $PKG/_variants/$1.so
