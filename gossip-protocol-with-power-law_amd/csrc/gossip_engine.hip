@@ -176,6 +176,7 @@ struct ExpandArgs {
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
   int32_t early_exit;                  // this round scans with the coverage check
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
+  int32_t near_done;                   // early-exit round with most messages held: fewer rows in flight
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
   const u64* __restrict__ cmk;         // compact-list masks of this round's senders (or null):
                                        //   0 = not a sender, CML_DENSE = full row, else the mask
@@ -365,9 +366,9 @@ __device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
 #ifndef GP_WORD_SKIP
 #define GP_WORD_SKIP 1
 #endif
-template <int W>
-__device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
-                                            u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
+template <int W, int RIF>
+__device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
+                                              u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
   constexpr int RPI = Geo<W>::RPI;
   bool live = true;   // this lane's words still miss messages
   if (GP_WORD_SKIP && ee) {
@@ -376,20 +377,20 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* 
     const u64x2 miss = want & ~t;
     live = (miss.x | miss.y) != 0ull;
   }
-  for (int k0 = 0; k0 < cnt; k0 += GP_ROWS_IN_FLIGHT * RPI) {
-    u64x2 r[GP_ROWS_IN_FLIGHT];
+  for (int k0 = 0; k0 < cnt; k0 += RIF * RPI) {
+    u64x2 r[RIF];
 #pragma unroll
-    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
+    for (int q = 0; q < RIF; ++q) {
       const int k = k0 + g + q * RPI;
       r[q] = u64x2{0, 0};
       if (k < cnt && live) r[q] = load_piece<W>(a.rows, idx[k], lw);
     }
 #pragma unroll
-    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
-    st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
+    for (int q = 0; q < RIF; ++q) acc |= r[q];
+    st.add(S_GATHERED, (u64)min(RIF * RPI, cnt - k0));
     u64 pieces = 0;   // 8 * WPL-byte pieces actually loaded (word skip)
 #pragma unroll
-    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) pieces += (u64)__popcll(__ballot(k0 + g + q * RPI < cnt && live));
+    for (int q = 0; q < RIF; ++q) pieces += (u64)__popcll(__ballot(k0 + g + q * RPI < cnt && live));
     st.add(S_ROW_BYTES, pieces * (u64)(8 * Geo<W>::WPL));
     if (ee) {
       u64x2 t = acc;
@@ -400,6 +401,21 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* 
     }
   }
   return false;
+}
+// near the end of a run (early exit, most messages held) receivers complete
+// after a few rows, and rows already in flight past that point are wasted:
+// gather 2 rows per lane at a time there (C4 round 4: 12.8 -> 10.4 ms, 67.2 ->
+// 64.6 ms per run same-box), the full GP_ROWS_IN_FLIGHT elsewhere
+template <int W>
+__device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
+                                            u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
+#ifndef GP_NEAR_DONE_OFF
+  if (GP_ROWS_IN_FLIGHT > 2 && a.near_done)
+#else
+  if (false)
+#endif
+    return gather_rows_n<W, 2>(a, idx, cnt, g, lw, acc, st, ee, want);
+  return gather_rows_n<W, GP_ROWS_IN_FLIGHT>(a, idx, cnt, g, lw, acc, st, ee, want);
 }
 
 // compact-row rounds: the staged senders' record masks into L.msk (one
@@ -2035,6 +2051,11 @@ static int launch_expand(Ctx* c) {
   ExpandArgs a{};
   fill_expand(c, a);
   a.unfiltered = c->unfiltered_now ? 1 : 0;
+  // (not with liveness: messages cut off by crashes keep the component targets
+  // out of reach, receivers scan to the end and want every row in flight --
+  // C5 rounds 5-6 56.8 -> 64.3 ms with the switch on)
+  a.near_done = c->early_exit_now && !c->liveness_active &&
+                (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m ? 1 : 0;
   switch (c->words) {
     case 1: launch_expand_w<1>(c, a); break;
     case 2: launch_expand_w<2>(c, a); break;
