@@ -409,12 +409,11 @@ __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t
 template <int W>
 __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
                                             u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
-#ifndef GP_NEAR_DONE_OFF
-  if (GP_ROWS_IN_FLIGHT > 2 && a.near_done)
-#else
-  if (false)
+#ifndef GP_NEAR_DONE_RIF
+#define GP_NEAR_DONE_RIF 2
 #endif
-    return gather_rows_n<W, 2>(a, idx, cnt, g, lw, acc, st, ee, want);
+  if (GP_ROWS_IN_FLIGHT > GP_NEAR_DONE_RIF && a.near_done)
+    return gather_rows_n<W, GP_NEAR_DONE_RIF>(a, idx, cnt, g, lw, acc, st, ee, want);
   return gather_rows_n<W, GP_ROWS_IN_FLIGHT>(a, idx, cnt, g, lw, acc, st, ee, want);
 }
 
