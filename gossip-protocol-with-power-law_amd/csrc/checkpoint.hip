@@ -55,6 +55,7 @@ static std::vector<Section> plain_sections(Ctx* c) {
       {c->d_deg_live, na * 4},
       {c->d_tbits, (na + 63) / 64 * 8},
       {c->d_msg_cov, W * 64 * 4 * 8},
+      {c->d_alive, 2 * W * 8},
       {c->d_done_at, na * 4},
       {c->d_cmask, (int64_t)c->cmask_rows * W * 8},
   };

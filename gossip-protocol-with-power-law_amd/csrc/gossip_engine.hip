@@ -177,6 +177,8 @@ struct ExpandArgs {
   int32_t early_exit;                  // this round scans with the coverage check
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
   int32_t near_done;                   // early-exit round with most messages held: fewer rows in flight
+  const u64* __restrict__ alive;       // [W] messages some sender forwards this round (or null)
+  u64* __restrict__ alive_next;        // [W] the same for round r + 1: OR of the new rows (or null)
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
   const u64* __restrict__ cmk;         // compact-list masks of this round's senders (or null):
                                        //   0 = not a sender, CML_DENSE = full row, else the mask
@@ -257,6 +259,7 @@ struct WaveLdsT {
   u64 cm[CML ? 64 : 1];           // compact-row rounds: mask word of the wave's vertex k (committed)
   int32_t pre[PRE ? 64 : 1][PRE_IDS];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
   uint8_t np[PRE ? 64 : 1];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
+  u64 alive[64];                  // OR of the new rows this wave wrote (alive_next)
 };
 using WaveLds = WaveLdsT<false, false>;
 #define LDS_OF(MODE) WaveLdsT<((MODE) & 3) == SCAN_PRE, ((MODE) & SCAN_CML) != 0>
@@ -265,6 +268,38 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Alive messages: F_r, the messages some sender forwards in
+// round r, is the OR of the rows received for the first time in round r - 1
+// plus the messages injected in round r.  A live receiver already holds every
+// bit of a sender's row outside its frontier (ExpandArgs), so nothing outside
+// F_r can be new to it and the early-exit target is cm & F_r & ~seen.  Under
+// churn this is what lets receivers stop when crashes cut a message off (the
+// component target cm then stays out of reach).  Each wave ORs its new rows
+// into LDS and flushes them once, skipping words the global row already has.
+template <int W, class LDS>
+__device__ __forceinline__ void alive_add(const ExpandArgs& a, LDS& L, int lw, u64x2 nw) {
+  constexpr int WPL = Geo<W>::WPL;
+  if (!a.alive_next) return;
+  if (nw.x) atomicOr(&L.alive[lw * WPL], nw.x);
+  if (WPL == 2 && nw.y) atomicOr(&L.alive[lw * WPL + 1], nw.y);
+}
+template <int W>
+__device__ __forceinline__ void alive_zero(const ExpandArgs& a, u64* alive, int lane) {
+  if (a.alive_next && lane < W) alive[lane] = 0ull;
+}
+template <int W>
+__device__ __forceinline__ void alive_flush(const ExpandArgs& a, const u64* alive, int lane) {
+  if (!a.alive_next) return;
+  wave_sync_lds();
+  if (lane < W) {
+    const u64 x = alive[lane];
+    if (x) {
+      const u64 cur = __hip_atomic_load(a.alive_next + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (x & ~cur) atomicOr(a.alive_next + lane, x);
+    }
+  }
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t x, int lane) {
@@ -320,7 +355,9 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
 // per-arc activity mask built by k_arcmask before the round, or no check at all
 // (unfiltered dense rounds)
 enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PRE = 3,
-                SCAN_CML = 4 /* flag: read / write compact Message-Lists (W = 64) */ };
+                SCAN_CML = 4 /* flag: read / write compact Message-Lists (W = 64) */,
+                SCAN_ALIVE = 8 /* flag: early-exit targets narrowed to the alive messages (k_expand);
+                                  a variant of its own: +2-3 VGPRs cost a wave per SIMD */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
@@ -486,14 +523,15 @@ __device__ __forceinline__ u64x2 load_seen(const ExpandArgs& a, int v, uint32_t 
 
 // early exit: park the receiver's seen row in LDS (finish_row reuses it) and
 // return, in group-0 lanes, the messages of its component it still lacks
-template <int W, class LDS>
+template <int W, class LDS, bool ALIVE = true>
 __device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, LDS& L, int g, int lw,
                                                    uint32_t sv_slot, int32_t mrow) {
   constexpr int WPL = Geo<W>::WPL;
   // every row slot group loads the same pieces (one fetch per line): each lane
   // needs its words' target to skip the loads of words already complete
   const u64x2 sv = load_seen<W>(a, v, sv_slot, lw);
-  const u64x2 cm = load_piece<W>(a.cmask, mrow, lw);
+  u64x2 cm = load_piece<W>(a.cmask, mrow, lw);
+  if (ALIVE && a.alive) cm &= load_piece<W>(a.alive, 0, lw);
   if (g == 0) {
     L.seen[lw * WPL] = sv.x;
     if constexpr (WPL == 2) L.seen[lw * WPL + 1] = sv.y;
@@ -644,6 +682,7 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
     if (a.cml_next) cm = write_cml(a.cml_next, v, g, lw, sv | nw);
   }
   if (g == 0) {
+    alive_add<W>(a, L, lw, nw);
     store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);   // the whole row: the slot may hold an older one
     if (a.frx_next) store_piece<W>(a.frx_next, v, lw, nw);
     if (a.first) {
@@ -723,6 +762,8 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
   auto& L = s_w[wib];
+  constexpr bool ALIVE = (MODE & SCAN_ALIVE) != 0;
+  constexpr int SCAN = MODE & ~SCAN_ALIVE;
   WaveStats st;
   ws_zero(st);
   const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
@@ -792,6 +833,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     st.add(S_VISITED, (u64)__popcll(__ballot(need)));
     L.tot[lane] = 0u;
     L.dig[lane] = 0ull;
+    alive_zero<W>(a, L.alive, lane);
     wave_sync_lds();
     const bool ee = a.early_exit != 0;
     u64 m = __ballot(need);
@@ -805,9 +847,12 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       u64x2 acc = {0, 0}, want = {0, 0};
       if (ee) {
         if (sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
-        want = early_exit_target<W>(a, v, L, g, lw, sv_slot, L.mi[k]);
+        want = early_exit_target<W, LDS_OF(MODE), ALIVE>(a, v, L, g, lw, sv_slot, L.mi[k]);
       }
-      if constexpr ((MODE & 3) == SCAN_PRE) {
+      // (with alive sets a receiver may hold every alive message of its
+      // component already: then there is nothing to scan)
+      if (ALIVE && ee && a.alive && !__any((want.x | want.y) != 0ull)) {
+      } else if constexpr ((MODE & 3) == SCAN_PRE) {
         const uint32_t np = L.np[k];
         bool done = false;
         if constexpr (W == 64 && (MODE & SCAN_CML) != 0) {
@@ -820,13 +865,14 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         }
         if (done) {
         } else if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);
-        else gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
+        else gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       } else {
-        gather_scan<W, MODE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
+        gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       }
       reduce_slots<W>(acc);
       finish_row<W, true, (MODE & SCAN_CML) != 0>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot, k);
     }
+    alive_flush<W>(a, L.alive, lane);
     commit_vertices(a, L, li, need, st);
   }
   flush_stats(st, a.partial);
@@ -869,6 +915,8 @@ struct FlatLds {
   uint32_t tot[NR];             // receiver side: new bits of receiver k
   u64 dig[NR];                  // its digest terms
   int8_t rd[NR];                // its seen row was read
+  u64 alive[W];                 // OR of the new rows this wave wrote (alive_next); W words, so
+                                // that W = 16 keeps 4 blocks per CU
 };
 
 // one flat pass: the arcs [start, start + sdeg) of every lane's receiver, as
@@ -1013,6 +1061,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
   ws_zero(st);
   const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * NR;
   if (base < a.nloc) {
+    alive_zero<W>(a, F.alive, lane);
     // per-lane state is reloaded (coalesced) where it is needed rather than
     // kept live across the passes: VGPRs are what bound this kernel's waves
     const int64_t li = base + lane;
@@ -1089,7 +1138,8 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
           accp.y = 0;
           if constexpr (WPL == 2) accp.y = F.acc[r][lw * WPL + 1];
           const u64x2 sv = rslot != SLOT_NONE ? load_piece<W>(a.slot[rslot], rv, lw) : u64x2{0, 0};
-          const u64x2 cm = load_piece<W>(a.cmask, rm, lw);
+          u64x2 cm = load_piece<W>(a.cmask, rm, lw);
+          if (a.alive) cm &= load_piece<W>(a.alive, 0, lw);
           const u64x2 m = cm & ~(sv | accp);
           miss = (m.x | m.y) != 0ull;
         }
@@ -1124,6 +1174,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       const uint32_t tot = group_sum<LPR>((uint32_t)(__popcll(nw.x) + __popcll(nw.y)));
       u64 t = 0;
       if (tot) {
+        alive_add<W>(a, F, lw, nw);
         store_piece<W>(a.slot[a.wslot], rv, lw, sv | nw);
         if (a.frx_next) store_piece<W>(a.frx_next, rv, lw, nw);
         if (a.first) {
@@ -1165,6 +1216,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
     st.add(S_WRITTEN, wave_sum_u64(nwritten));
     st.add(S_NEXT_ARCS, wave_sum_u64(narcs));
     st.add(S_SEEN_READ, wave_sum_u64(nseen));
+    alive_flush<W>(a, F.alive, lane);
   }
   flush_stats(st, a.partial);
 }
@@ -1209,6 +1261,8 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
   WaveStats st;
   ws_zero(st);
   const int64_t h = (int64_t)blockIdx.x * WAVES + wib;
+  alive_zero<W>(a, s_w[wib].alive, lane);
+  wave_sync_lds();
   if (h < a.n_items) {
     const int v = a.hubs[h];
     const int64_t i = v - a.vbegin;
@@ -1228,6 +1282,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
       finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
     }
   }
+  alive_flush<W>(a, s_w[wib].alive, lane);
   flush_stats(st, a.partial);
 }
 
@@ -1425,6 +1480,8 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
   ws_zero(st);
   const int64_t nt = (int64_t)a.stats[S_TOUCH_CURSOR];
   const int64_t stride = (int64_t)gridDim.x * WAVES;
+  alive_zero<W>(a, s_w[wib].alive, lane);
+  wave_sync_lds();
   for (int64_t k = (int64_t)blockIdx.x * WAVES + wib; k < nt; k += stride) {
     const int32_t v = a.touched[k];
     const int64_t i = v - a.vbegin;
@@ -1436,6 +1493,7 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
     st.add(S_VISITED, 1);
     finish_row<W, false, false>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
   }
+  alive_flush<W>(a, s_w[wib].alive, lane);
   flush_stats(st, a.partial);
 }
 
@@ -1609,6 +1667,7 @@ struct InjectArgs {
   uint32_t* __restrict__ fpop;
   u64* __restrict__ frx;               // exact frontier rows (track_msg_forwards only)
   u64* __restrict__ cmk;               // compact-list masks of slot r & 1 (or null)
+  u64* __restrict__ alive;             // [W] alive messages of round r (or null)
   uint32_t* __restrict__ seenpop;
   uint8_t* __restrict__ first;
   u64* __restrict__ digest;
@@ -1648,6 +1707,7 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
         if (a.frx) a.frx[(size_t)o * a.words + lane] = f | b;
       }
       if (a.cmk && lane == 0) a.cmk[o] = CML_DENSE;   // a sender this round, read as a full row
+      if (a.alive && b) atomicOr(a.alive + lane, b);   // injected messages are forwarded this round
       const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
       if (lane == 0) {
         a.fpop[o] = fp + nb;
@@ -1875,7 +1935,15 @@ static int grid_for(int64_t work, int64_t per_block) {
   return (int)g;
 }
 
+// alive sets need every receiver of the round in this context: single-rank
+// contexts (one GPU, message shards); off for vertex partitions.  Only with
+// liveness: without crashes a message stops only once its whole component
+// holds it, so F_r never narrows cm & ~seen and the bookkeeping is pure cost
+static bool alive_on(const Ctx* c) { return c->nranks == 1 && c->d_alive != nullptr && c->liveness_active; }
+
 static void fill_expand(Ctx* c, ExpandArgs& a) {
+  a.alive = alive_on(c) ? c->d_alive + (size_t)c->cur * c->words : nullptr;
+  a.alive_next = alive_on(c) ? c->d_alive + (size_t)(c->cur ^ 1) * c->words : nullptr;
   a.row_ptr = c->d_row_ptr;
   a.col = c->d_col;
   a.rows = c->d_slot[c->cur];
@@ -1985,10 +2053,26 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
         else
           hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_CML>), grid, dim3(BLOCK), 0, c->stream, a);
       }
-    } else if (c->prefilter_now)
-      hipLaunchKernelGGL((k_expand<W, SCAN_PRE>), grid, dim3(BLOCK), 0, c->stream, a);
-    else
-      hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+    } else {
+      // early-exit rounds with alive sets (liveness) take the SCAN_ALIVE
+      // variants; instantiated for the widths the per-receiver kernel runs by
+      // default (narrower rows take the flat kernel)
+      bool done = false;
+      if constexpr (W >= 32) {
+        if (a.alive && a.early_exit) {
+          if (c->prefilter_now)
+            hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
+          else
+            hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
+          done = true;
+        }
+      }
+      if (done) {
+      } else if (c->prefilter_now)
+        hipLaunchKernelGGL((k_expand<W, SCAN_PRE>), grid, dim3(BLOCK), 0, c->stream, a);
+      else
+        hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+    }
   }
   (void)hipEventRecord(c->ev[5], c->stream);
   if (c->n_hub_items > 0) {
@@ -2005,6 +2089,8 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 }
 
 static int launch_expand(Ctx* c) {
+  if (alive_on(c))   // F_{r+1} is built by this round's receivers
+    GP_HIP(hipMemsetAsync(c->d_alive + (size_t)(c->cur ^ 1) * c->words, 0, (size_t)c->words * 8, c->stream));
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
                      dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc);
   // direction: push when the senders' arcs are a small share of all arcs
@@ -2148,7 +2234,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
-  dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt);
+  dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
   c->d_msg_fwd = nullptr;
@@ -2228,7 +2314,8 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_touched, na));
   GP_TRY(dalloc(&c->d_active, na));
   GP_TRY(dalloc(&c->d_big, na));
-  GP_TRY(dalloc(&c->d_msg_cov, W * 64 * 4));   // [local cov | local fwd | global cov | global fwd]
+  GP_TRY(dalloc(&c->d_msg_cov, W * 64 * 4));
+  GP_TRY(dalloc(&c->d_alive, 2 * W));   // [local cov | local fwd | global cov | global fwd]
   c->d_msg_fwd = c->d_msg_cov + W * 64;
   c->report_cap = std::max<int64_t>(c->cfg.report_capacity, 1);
   GP_TRY(dalloc(&c->d_reports, (size_t)c->report_cap));
@@ -2379,7 +2466,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
   dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
-  dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt);
+  dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -2608,6 +2695,7 @@ int gp_reset(gp_ctx* c) {
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
   GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToDevice, s));
   GP_HIP(hipMemsetAsync(c->d_msg_cov, 0, W * 64 * 4 * 8, s));
+  GP_HIP(hipMemsetAsync(c->d_alive, 0, 2 * W * 8, s));
   GP_HIP(hipMemsetAsync(c->d_stats, 0, (64 + (size_t)NPART * NST) * 8, s));
   c->cur = 0;
   c->round = 0;
@@ -2698,6 +2786,7 @@ static int round_launch(Ctx* c) {
     ia.fpop = c->d_fpop[c->cur];
     ia.frx = c->d_frx[0] ? c->d_frx[c->cur] : nullptr;
     ia.cmk = c->d_cmk[0] ? c->d_cmk[c->cur] : nullptr;
+    ia.alive = alive_on(c) ? c->d_alive + (size_t)c->cur * c->words : nullptr;
     ia.seenpop = c->d_seenpop;
     ia.first = c->cfg.track_first ? c->d_first : nullptr;
     ia.digest = c->cfg.track_digest ? c->d_digest : nullptr;

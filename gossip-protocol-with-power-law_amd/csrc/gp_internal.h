@@ -128,6 +128,7 @@ struct Ctx {
   bool done_dirty = false;          // the working targets differ from the pristine ones
   u64* d_msg_cov = nullptr;    // [W*64]
   u64* d_msg_fwd = nullptr;    // [W*64]
+  u64* d_alive = nullptr;      // [2][W] alive messages per round parity
   gp_report* d_reports = nullptr;
   int64_t report_cap = 0;
   u64* d_stats = nullptr;      // [NSTAT]

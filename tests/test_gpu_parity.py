@@ -289,15 +289,17 @@ def test_wide_rows_churn(pkg, oracle, mode):
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
-def test_lost_messages_drop_from_targets(pkg, oracle, mode):
+@pytest.mark.parametrize("m", [4096, 2048])
+def test_lost_messages_drop_from_targets(pkg, oracle, mode, m):
     """Messages whose origin is down at the inject round are dropped from the
     early-exit targets of their component for that run (k_lost_clear,
-    k_done_fix): the run stays bit-exact, and gp_reset restores the targets, so
-    repeated runs on one context are identical."""
+    k_done_fix), and late rounds narrow the targets to the alive messages
+    (SCAN_ALIVE variants at W = 64 and 32): the run stays bit-exact, and
+    gp_reset restores the targets, so repeated runs on one context are
+    identical."""
     push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     rp, col = oracle.chung_lu(40_000, 10, 2.4, 23)
     g = pkg.CSR(40_000, rp, col, False)
-    m = 4096
     origin = pkg.overlay.random_origins(g.n, m, seed=23)
     inject = (np.arange(m) % 5).astype(np.int32)
     crashes = [(int(v), int(r)) for v, r in zip(origin[:300], inject[:300])]   # down when injected
