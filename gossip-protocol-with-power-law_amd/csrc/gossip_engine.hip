@@ -2017,7 +2017,17 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   if (a.unfiltered)
     hipLaunchKernelGGL(k_fixup_rows<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
                        c->d_abits, c->d_ws, c->d_slot[c->cur], c->cur, c->n_alloc);
-  const bool flat = W <= 32 && W <= c->cfg.flat_max_words;
+  // W = 32 rows take the per-receiver kernel, except in dense near-done rounds
+  // (most messages held, last round's new bits >= m/4 per vertex): there the
+  // flat kernel's 2-arc prefix pass completes most receivers from their hub
+  // rows (2048-message shard round 4: 10.2 -> 6.6 ms; round 5, with m/16,
+  // went 3.2 -> 4.2 ms, hence m/4)
+#ifndef GP_FLAT_NEAR_DONE
+#define GP_FLAT_NEAR_DONE 1
+#endif
+  const bool flat_nd = GP_FLAT_NEAR_DONE && W == 32 && c->cfg.flat_max_words > 0 && a.near_done &&
+                       (double)c->prev_new_bits * 4.0 >= (double)c->n * (double)c->m;
+  const bool flat = W <= 32 && (W <= c->cfg.flat_max_words || flat_nd);
   const bool masked = !a.unfiltered && !flat && c->arc_mask_now;
   if (masked) {   // mask words of the owned vertices' in-arcs
     const int64_t kb = c->h_row_ptr[(size_t)c->vbegin] >> 6;
