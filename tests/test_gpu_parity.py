@@ -435,10 +435,13 @@ def test_compact_message_lists(pkg, oracle, prefilter):
 
 
 @pytest.mark.parametrize("shards", [2, 4])
-def test_message_shards_match_whole_run(pkg, shards):
+@pytest.mark.parametrize("churn", [False, True])
+def test_message_shards_match_whole_run(pkg, shards, churn):
     """Message shards on one GPU, one context each: the per-round
     sends and new bits add up to the whole run's, coverage / forwards / first
-    columns concatenate, and the shard digests XOR to the whole run's digest."""
+    columns concatenate, and the shard digests XOR to the whole run's digest.
+    With churn every shard draws the same crashes and reports (liveness is
+    replicated) and runs its own alive sets."""
     rp, col = pkg_oracle_chung_lu(20_000, 8, 2.4, 13)
     g = pkg.CSR(20_000, rp, col, False)
     m = 1024
@@ -446,7 +449,8 @@ def test_message_shards_match_whole_run(pkg, shards):
     inject = (np.arange(m) % 3).astype(np.int32)
 
     def run(lo, hi):
-        eng = pkg.GossipEngine(0, track_first=1, track_digest=1)
+        cfg = dict(churn=1, p_fail=0.02, churn_seed=7, track_msg_forwards=1) if churn else {}
+        eng = pkg.GossipEngine(0, track_first=1, track_digest=1, **cfg)
         eng.load_graph(g)
         eng.set_message_shard(origin, inject, lo, hi)
         eng.reset()
@@ -461,6 +465,12 @@ def test_message_shards_match_whole_run(pkg, shards):
     for i, s in enumerate(whole[0]):
         for k in ("new_bits", "sends", "injected"):
             assert s[k] == sum(p[0][i][k] if i < len(p[0]) else 0 for p in parts), (k, i)
+        for p in parts:
+            if i < len(p[0]):
+                for k in ("crashed", "reports", "removals"):
+                    assert p[0][i][k] == s[k], (k, i)
+    if churn:
+        assert sum(s["removals"] for s in whole[0]) > 0
     assert np.array_equal(np.concatenate([p[1] for p in parts], axis=1), whole[1])
     dig = np.zeros_like(whole[2])
     for p in parts:
