@@ -240,7 +240,9 @@ def main():
                        "setup_s": round(setup_s, 2)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": f"k_expand<{eng.words}>, HIP events on the engine stream",
+                         "kernel": (f"k_expand<{eng.words}>" if eng.words > 32 else
+                                    f"k_expand<{eng.words}> / k_expand_flat<{eng.words}>")
+                                   + ", HIP events on the engine stream",
                          "launches": len(pulls),
                          "avg_launch_ms": kern_ms / max(len(pulls), 1),
                          "alg_bytes_per_launch": nbytes / max(len(pulls), 1),
