@@ -1756,46 +1756,108 @@ struct LiveArgs {
   int32_t r;
 };
 
-// The detection candidates are appended with one cursor add per wave (a
-// ballot and lane ranks): ~1 % of n reach the miss threshold every round, and
-// one same-address atomic each serialised k_churn at 4.7 ms on C5.
+// Four vertices per lane: state and miss bytes move as 32-bit words (a wave
+// covers 256 vertices per instruction) and are stored only when they change.
+// Detection candidates (~1 % of n every round under C5 churn) collect in an
+// LDS list per block and reach the global list with one cursor add per block:
+// a same-address add per candidate, or per wave, serialised k_churn at
+// 4.7-5.9 ms per round on C5 (~0.5 M adds at ~12 ns).
+constexpr int CHURN_CAND_LDS = 2048;
 __global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
+  __shared__ int32_t s_cand[CHURN_CAND_LDS];
+  __shared__ uint32_t s_ncand;
+  __shared__ u64 s_base;
   WaveStats st;
   ws_zero(st);
+  if (threadIdx.x == 0) s_ncand = 0u;
+  __syncthreads();
   u64 ncrash = 0;
-  const int lane = threadIdx.x & 63;
+  const int64_t nw = (a.n + 3) >> 2;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
-  for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < a.n; v0 += stride) {
-    const int64_t v = v0 + lane;   // the whole wave iterates together (ballot below)
-    bool is_cand = false;
-    if (v < a.n) {
-      uint8_t s = a.state[v];
-      if (!(s & ST_DOWN)) {
-        bool crash = (s & ST_PENDING) != 0;
-        if (!crash && (a.p_always || a.p_thresh))
-          crash = a.p_always || draw(a.crash_key, (u64)v) < a.p_thresh;
-        if (crash) {
-          s = (uint8_t)((s | ST_CRASHED) & ~ST_PENDING);
-          a.fpop[v] = 0;   // crash-stop: its frontier is never sent
-          if (v >= a.vbegin && v < a.vend) ncrash += 1;
+  for (int64_t w0 = (int64_t)blockIdx.x * BLOCK; w0 < nw; w0 += stride) {
+    const int64_t w = w0 + threadIdx.x;
+    const int64_t v0 = w << 2;
+    const bool full = v0 + 4 <= a.n;
+    uint32_t cand = 0;   // bit q: vertex v0 + q reached the miss threshold
+    if (w < nw) {
+      uint32_t sw = 0;
+      if (full) {
+        sw = reinterpret_cast<const uint32_t*>(a.state)[w];
+      } else {
+        for (int q = 0; q < 4; ++q)
+          if (v0 + q < a.n) sw |= (uint32_t)a.state[v0 + q] << (8 * q);
+      }
+      uint32_t nsw = sw;
+      bool anyc = false;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t v = v0 + q;
+        uint8_t s = (uint8_t)(sw >> (8 * q));
+        if (v < a.n && !(s & ST_DOWN)) {
+          bool crash = (s & ST_PENDING) != 0;
+          if (!crash && (a.p_always || a.p_thresh))
+            crash = a.p_always || draw(a.crash_key, (u64)v) < a.p_thresh;
+          if (crash) {
+            s = (uint8_t)((s | ST_CRASHED) & ~ST_PENDING);
+            a.fpop[v] = 0;   // crash-stop: its frontier is never sent
+            if (v >= a.vbegin && v < a.vend) ncrash += 1;
+          }
+        }
+        anyc |= (s & ST_CRASHED) != 0;
+        nsw = (nsw & ~(0xFFu << (8 * q))) | ((uint32_t)s << (8 * q));
+      }
+      if (anyc) {   // heartbeat misses of the crashed vertices
+        uint32_t mw = 0;
+        if (full) {
+          mw = reinterpret_cast<const uint32_t*>(a.miss)[w];
+        } else {
+          for (int q = 0; q < 4; ++q)
+            if (v0 + q < a.n) mw |= (uint32_t)a.miss[v0 + q] << (8 * q);
+        }
+        uint32_t nmw = mw;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint8_t s = (uint8_t)(nsw >> (8 * q));
+          if (!(s & ST_CRASHED)) continue;
+          uint32_t mi = (mw >> (8 * q)) & 0xFFu;
+          if (mi < 255) ++mi;
+          nmw = (nmw & ~(0xFFu << (8 * q))) | (mi << (8 * q));
+          if ((int)mi == a.miss_thr && !(s & ST_REMOVED)) cand |= 1u << q;
+        }
+        if (nmw != mw) {
+          if (full) {
+            reinterpret_cast<uint32_t*>(a.miss)[w] = nmw;
+          } else {
+            for (int q = 0; q < 4; ++q)
+              if (v0 + q < a.n) a.miss[v0 + q] = (uint8_t)(nmw >> (8 * q));
+          }
         }
       }
-      if (s & ST_CRASHED) {
-        uint32_t mi = a.miss[v];
-        if (mi < 255) ++mi;
-        a.miss[v] = (uint8_t)mi;
-        is_cand = (int)mi == a.miss_thr && !(s & ST_REMOVED);
+      if (nsw != sw) {
+        if (full) {
+          reinterpret_cast<uint32_t*>(a.state)[w] = nsw;
+        } else {
+          for (int q = 0; q < 4; ++q)
+            if (v0 + q < a.n) a.state[v0 + q] = (uint8_t)(nsw >> (8 * q));
+        }
       }
-      a.state[v] = s;
     }
-    const u64 cm = __ballot(is_cand);
-    if (cm) {
-      u64 base = 0;
-      if (lane == 0) base = atomicAdd(&a.stats[S_CAND], (u64)__popcll(cm));
-      base = __shfl(base, 0);
-      if (is_cand) a.cand[base + (u64)lane_rank(cm)] = (int32_t)v;
+    for (int q = 0; q < 4; ++q) {
+      if (!((cand >> q) & 1u)) continue;
+      const uint32_t k = atomicAdd(&s_ncand, 1u);
+      if (k < (uint32_t)CHURN_CAND_LDS) {
+        s_cand[k] = (int32_t)(v0 + q);
+      } else {   // list full (p_fail near 1): straight to the global list
+        const u64 slot = atomicAdd(&a.stats[S_CAND], 1ull);
+        a.cand[slot] = (int32_t)(v0 + q);
+      }
     }
   }
+  __syncthreads();
+  const uint32_t nl = min(s_ncand, (uint32_t)CHURN_CAND_LDS);
+  if (threadIdx.x == 0 && nl) s_base = atomicAdd(&a.stats[S_CAND], (u64)nl);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < nl; k += BLOCK) a.cand[s_base + k] = s_cand[k];
   // crash counts differ per lane: wave-reduce, then one uniform add
   u64 c = ncrash;
 #pragma unroll
