@@ -14,6 +14,7 @@ libgossip_hip.so, torch.distributed/gloo only distributes the RCCL id and the
 timings).
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -93,22 +94,24 @@ def round_bytes(st, words, nloc):
             + w8 * st["rows_written"])
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+PMC_TRAFFIC = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json")))
 
 
 def pmc_traffic(config):
     """HBM traffic per k_expand launch measured by the two rocprofv3 --pmc
     passes of scripts/gpu_round_profile.sh (FETCH_SIZE x2 + WRITE_SIZE, the
-    gfx950 correction of MI355X_MICROARCH.md), for this exact workload; None
-    when no such measurement is committed under profiles/."""
-    try:
-        d = json.load(open(PMC_TRAFFIC))
-    except (OSError, ValueError):
-        return None, None
+    gfx950 correction of MI355X_MICROARCH.md), from the profiles/pmc_traffic*.json
+    whose workload keys match this run (C4: pmc_traffic.json, C5:
+    pmc_traffic_c5.json); None when no such measurement is committed."""
     keys = ("n", "arcs", "messages", "words_per_row", "seed", "parallelism")
-    if any(d["config"].get(k) != config.get(k) for k in keys):
-        return None, None
-    return d["traffic_bytes_per_launch"], os.path.relpath(PMC_TRAFFIC, ROOT)
+    for path in PMC_TRAFFIC:
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if all(d["config"].get(k) == config.get(k) for k in keys):
+            return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def dense_round_bytes(n, nnz, words):
