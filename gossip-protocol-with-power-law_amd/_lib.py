@@ -83,6 +83,7 @@ class Config(ctypes.Structure):
         ("unfiltered_pct", ctypes.c_int32),
         ("msg_word_base", ctypes.c_int32),
         ("flat_max_words", ctypes.c_int32),
+        ("summary_min_n", ctypes.c_int64),
     ]
 
 

@@ -171,6 +171,7 @@ struct ExpandArgs {
   uint8_t* __restrict__ ws;            // [n_alloc] bit p: slot p written this run
   const uint32_t* __restrict__ fpop;   // |frontier_r|: bits received in round r - 1 (+ injected)
   const u64* __restrict__ abits;       // bit v: fpop(v) != 0 (2 MB at 2^24)
+  const u64* __restrict__ sbits;       // bit k: abits[k] != 0 (sparse probe rounds of big overlays; else null)
   const int32_t* __restrict__ gcol;    // in-CSR columns in gather order (neighbour degree desc)
   const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
@@ -229,6 +230,12 @@ constexpr int CML_WORDS = 16;
 constexpr u64 CML_DENSE = ~0ull;
 
 // occupancy target of k_expand (waves per SIMD; 0 = compiler's choice)
+#ifndef GP_SUMMARY_PROBE
+#define GP_SUMMARY_PROBE 1
+#endif
+#ifndef GP_SUMMARY_RATIO
+#define GP_SUMMARY_RATIO 256.0
+#endif
 #ifndef GP_EXPAND_WAVES
 #define GP_EXPAND_WAVES 0
 #endif
@@ -800,6 +807,16 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
               u64 w[PRE_IDS];
 #pragma unroll
               for (int q = 0; q < PRE_IDS; ++q) c[q] = h * PRE_IDS + q < deg ? a.gcol[b + h * PRE_IDS + q] : -1;
+#if GP_SUMMARY_PROBE
+              if (a.sbits) {   // summary level first: L2-resident, most probes end there
+                u64 sw[PRE_IDS];
+#pragma unroll
+                for (int q = 0; q < PRE_IDS; ++q) sw[q] = c[q] >= 0 ? a.sbits[c[q] >> 12] : 0ull;
+#pragma unroll
+                for (int q = 0; q < PRE_IDS; ++q)
+                  w[q] = ((sw[q] >> ((c[q] >> 6) & 63)) & 1ull) ? a.abits[c[q] >> 6] : 0ull;
+              } else
+#endif
 #pragma unroll
               for (int q = 0; q < PRE_IDS; ++q) w[q] = c[q] >= 0 ? a.abits[c[q] >> 6] : 0ull;
 #pragma unroll
@@ -995,6 +1012,17 @@ __device__ __forceinline__ u64 flat_pass(const ExpandArgs& a, FlatLds<W>& F, int
         if constexpr (MODE != SCAN_UNFILTERED)
           if (col[q] >= 0) raw[q] = a.abits[col[q] >> 6];
       }
+#if GP_SUMMARY_PROBE
+      if constexpr (MODE != SCAN_UNFILTERED)
+        if (a.sbits) {
+          u64 sw[QA];
+#pragma unroll
+          for (int q = 0; q < QA; ++q) sw[q] = col[q] >= 0 ? a.sbits[col[q] >> 12] : 0ull;
+#pragma unroll
+          for (int q = 0; q < QA; ++q)
+            raw[q] = ((sw[q] >> ((col[q] >> 6) & 63)) & 1ull) ? a.abits[col[q] >> 6] : 0ull;
+        }
+#endif
 #pragma unroll
       for (int q = 0; q < QA; ++q) {
         const int32_t u = (col[q] >= 0 && ((raw[q] >> (col[q] & 63)) & 1ull)) ? col[q] : -1;
@@ -1507,6 +1535,16 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
     const u64 m = __ballot(v < n && fpop[v] != 0u);
     if (lane == 0) abits[v0 >> 6] = m;
   }
+}
+
+// summary level of the activity bitmap: bit j of sbits[k] = (abits[64k + j] != 0)
+__global__ __launch_bounds__(BLOCK) void k_mksum(const u64* __restrict__ abits, u64* __restrict__ sbits,
+                                                 int64_t nwords) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  const int64_t w = k * 64 + lane;
+  const u64 m = __ballot(w < nwords && abits[w] != 0ull);
+  if (lane == 0 && k * 64 < nwords) sbits[k] = m;
 }
 
 // per-arc activity mask of a filtered pull round: bit j of
@@ -2053,6 +2091,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.ws = c->d_ws;
   a.fpop = c->d_fpop[c->cur];
   a.abits = c->d_abits;
+  a.sbits = c->sum_now ? c->d_sbits : nullptr;
   a.amask = c->d_amask;
   a.cmk = c->cml_read_now ? c->d_cmk[c->cur] : nullptr;
   a.cml = c->cml_read_now ? c->d_cml[c->cur] : nullptr;
@@ -2227,6 +2266,19 @@ static int launch_expand(Ctx* c) {
   // first (pays once the probes are many: senders >= arc_mask_permille of n)
   c->arc_mask_now = !c->mode_push && !c->unfiltered_now && c->cfg.arc_mask_permille > 0 &&
                     senders * 1000.0 >= (double)c->cfg.arc_mask_permille * (double)c->n;
+  // summary probes: filtered rounds of overlays whose activity bitmap outgrows
+  // an XCD's L2, while few enough vertices send that most summary bits are 0
+  c->sum_now = false;
+#if GP_SUMMARY_PROBE
+  if (!c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.summary_min_n > 0 &&
+      c->n_alloc >= c->cfg.summary_min_n &&
+      senders * GP_SUMMARY_RATIO <= (double)c->n) {
+    const int64_t nwords = (c->n_alloc + 63) / 64;
+    hipLaunchKernelGGL(k_mksum, dim3(grid_for((nwords + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
+                       c->d_abits, c->d_sbits, nwords);
+    c->sum_now = true;
+  }
+#endif
   // compact Message-Lists (W = 64): written while the rows are sparse (last
   // round's receivers got <= CML_AVG_BITS new bits on average), read by a
   // filtered pull whose senders all wrote theirs in the previous round
@@ -2342,7 +2394,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_sp); dfree(&c->d_ws);
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
@@ -2400,6 +2452,9 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_deg_live, na));
   GP_TRY(dalloc(&c->d_cand, na));
   GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
+#if GP_SUMMARY_PROBE
+  GP_TRY(dalloc(&c->d_sbits, (na + 4095) / 4096));
+#endif
   // compact Message-Lists: 2 x 128 B per vertex, single-rank W = 64 runs only
   if (c->cfg.compact_rows && W == 64 && c->nranks == 1) {
     GP_TRY(dalloc(&c->d_cml[0], na * CML_WORDS));
@@ -2538,6 +2593,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->unfiltered_pct = 90;
   cfg->msg_word_base = 0;
   cfg->flat_max_words = 16;
+  cfg->summary_min_n = 1ll << 25;   // activity bitmap > 4 MB: outgrows an XCD's L2
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -2574,7 +2630,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
@@ -2600,6 +2656,7 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->report_capacity < 0) return set_error(GP_EINVAL, "report_capacity < 0");
   if (cfg->msg_word_base < 0) return set_error(GP_EINVAL, "msg_word_base < 0");
   if (cfg->prefilter_pct < 0) return set_error(GP_EINVAL, "prefilter_pct < 0");
+  if (cfg->summary_min_n < 0) return set_error(GP_EINVAL, "summary_min_n < 0");
   if (cfg->compact_rows != 0 && cfg->compact_rows != 1) return set_error(GP_EINVAL, "compact_rows must be 0 or 1");
   if (cfg->arc_mask_permille < 0) return set_error(GP_EINVAL, "arc_mask_permille < 0");
   GP_HIP(hipSetDevice(c->device));

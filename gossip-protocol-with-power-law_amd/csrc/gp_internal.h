@@ -85,6 +85,7 @@ struct Ctx {
   int32_t* d_cand = nullptr;        // [n] detection candidates of a round
   // [n_alloc/64] frontier_r activity bitmap (fpop != 0): 2 MB at 2^24
   u64* d_abits = nullptr;
+  u64* d_sbits = nullptr;   // summary level of d_abits (GP_SUMMARY_PROBE builds)
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
   u64* d_amask = nullptr;
   // push (sparse-round) mode
@@ -102,6 +103,7 @@ struct Ctx {
   u64 held_bits = 0;                // messages held so far, summed over vertices (global)
   bool unfiltered_now = false;      // this round's pull skips the activity check
   bool arc_mask_now = false;        // this round's filtered pull reads the per-arc mask
+  bool sum_now = false;             // this round's probes read the summary level first (GP_SUMMARY_PROBE)
   bool prefilter_now = false;       // this round's filtered pull probes low-degree in-lists lane-parallel
   // compact Message-Lists: 128-B records per vertex, per slot
   u64* d_cml[2] = {nullptr, nullptr};   // [n_alloc][16] records

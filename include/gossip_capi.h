@@ -124,6 +124,10 @@ typedef struct gp_config {
                                   global word indices, so shard digests XOR together     */
   int32_t flat_max_words;      /* rows of at most this many words (<= 32) take the
                                   edge-parallel pull kernel (0 = never)  */
+  int64_t summary_min_n;       /* filtered probe rounds of overlays with >= this many
+                                  vertices, with at most n/256 senders, probe a summary
+                                  level (1 bit per 64 vertices) before the activity
+                                  bitmap (0 = never)                    */
 } gp_config;
 
 /* what for gp_read */

@@ -37,13 +37,15 @@ MODE_IDS = ["pull", "pull-masked", "pull-unfiltered", "push", "adaptive"]
 
 def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096,
              push_ratio=10.0, unfiltered_pct=90, flat_max_words=16, arc_mask_permille=10, prefilter_pct=20,
-             compact_rows=1, **kw):
+             compact_rows=1, summary_min_n=None, **kw):
     churn = kw.get("churn", False)
     cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(bool(churn or crashes)),
                churn=int(churn), p_fail=kw.get("p_fail", 0.0), churn_seed=kw.get("churn_seed", 0),
                hub_threshold=hub_threshold, push_ratio=push_ratio,
                unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words,
                arc_mask_permille=arc_mask_permille, prefilter_pct=prefilter_pct, compact_rows=compact_rows)
+    if summary_min_n is not None:
+        cfg["summary_min_n"] = summary_min_n
     eng = _engine(pkg, g, origin, inject, **cfg)
     by_round = {}
     for v, r in crashes:
@@ -483,3 +485,21 @@ def test_message_shards_match_whole_run(pkg, shards, churn):
 def pkg_oracle_chung_lu(n, dbar, gamma, seed):
     from oracle import lib as oracle
     return oracle.chung_lu(n, dbar, gamma, seed)
+
+
+@pytest.mark.parametrize("prefilter", [0, 20])
+@pytest.mark.parametrize("churn", [False, True])
+def test_summary_probes(pkg, oracle, prefilter, churn):
+    """Summary-level activity probes (one bit per 64 vertices read before the
+    bitmap word) forced on at any size: sparse filtered pull rounds, with and
+    without the lane-parallel prefilter, per-receiver kernel, with churn."""
+    rp, col = oracle.chung_lu(200_000, 8, 2.5, 21)
+    g = pkg.CSR(200_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 256, seed=21)
+    inject = (np.arange(256) % 6).astype(np.int32)
+    kw = dict(churn=True, p_fail=0.01, churn_seed=5) if churn else {}
+    r = _compare(pkg, oracle, g, origin, inject, push_ratio=0.0, flat_max_words=0, arc_mask_permille=0,
+                 prefilter_pct=prefilter, compact_rows=0, summary_min_n=1, **kw)
+    # the summary path runs in filtered pull rounds with <= n/256 senders
+    assert any(s["mode"] == 0 and s["scan"] != 2 and s["active"] * 256 <= g.n for s in r["stats"])
+    r["eng"].close()
