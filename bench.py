@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--p-fail", type=float, default=0.01, help="c5: per-round crash probability")
     ap.add_argument("--hub-threshold", type=int, default=4096)
-    ap.add_argument("--push-ratio", type=float, default=400.0)
+    ap.add_argument("--push-ratio", type=float, default=100.0)
     ap.add_argument("--early-exit", type=int, default=1)
     ap.add_argument("--unfiltered-pct", type=int, default=90,
                     help="pull without the per-arc activity check when >= this %% of vertices send (0 = never)")

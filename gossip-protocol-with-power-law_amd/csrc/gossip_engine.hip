@@ -2585,7 +2585,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->miss_threshold = 3;     // 2 missed heartbeats + 1 unanswered PING (Peer.py:299-311)
   cfg->hub_threshold = 4096;
   cfg->report_capacity = 1 << 20;
-  cfg->push_ratio = 400.0;   // push when sender arcs <= nnz / 400
+  cfg->push_ratio = 100.0;   // push when sender arcs <= nnz / 100
   cfg->early_exit = 1;
   cfg->arc_mask_permille = 0;   // per-arc mask off: its build costs what it saves
   cfg->prefilter_pct = 20;
