@@ -230,6 +230,9 @@ constexpr int CML_WORDS = 16;
 constexpr u64 CML_DENSE = ~0ull;
 
 // occupancy target of k_expand (waves per SIMD; 0 = compiler's choice)
+#ifndef GP_DETECT_BLOCKS_PER_CU
+#define GP_DETECT_BLOCKS_PER_CU 16   // 4 -> 16: C5 304.1-304.5 -> 302.2-302.4 ms per run same-box
+#endif
 #ifndef GP_SUMMARY_PROBE
 #define GP_SUMMARY_PROBE 1
 #endif
@@ -2933,7 +2936,7 @@ static int round_launch(Ctx* c) {
     la.miss_thr = c->cfg.miss_threshold;
     la.r = r;
     hipLaunchKernelGGL(k_churn, dim3(std::min(grid_for(c->n, BLOCK), c->cu_count * 8)), dim3(BLOCK), 0, s, la);
-    hipLaunchKernelGGL(k_detect, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, la);
+    hipLaunchKernelGGL(k_detect, dim3(c->cu_count * GP_DETECT_BLOCKS_PER_CU), dim3(BLOCK), 0, s, la);
     GP_HIP(hipGetLastError());
     c->pending_crash = false;
   }
