@@ -80,6 +80,21 @@ class GossipEngine:
         check(self._lib.gp_read(self._ctx, _lib.COL, _ptr(col), col.nbytes))
         return CSR(n, rp, col, False)
 
+    def degrees(self):
+        """Degree of every vertex of the loaded overlay (in-degree of the
+        in-CSR; = degree for undirected overlays), from row_ptr alone."""
+        n = self.info()[0]
+        rp = np.empty(n + 1, dtype=np.int64)
+        check(self._lib.gp_read(self._ctx, _lib.ROW_PTR, _ptr(rp), rp.nbytes))
+        return np.diff(rp)
+
+    def check_degree(self, gamma, tol=0.15):
+        """SURVEY.md §8a A9 on the overlay this context holds: discrete MLE
+        gamma_hat with KS-chosen kmin against the generator's gamma (the
+        reference's intent, degree-weighted selection, demonstrate_powerlaw.py:19-27)."""
+        from . import degree
+        return degree.check_powerlaw(self.degrees(), gamma, tol)
+
     def info(self):
         n, nnz = ctypes.c_int64(), ctypes.c_int64()
         m, w = ctypes.c_int32(), ctypes.c_int32()
