@@ -168,7 +168,12 @@ class ProtocolBridge:
         new = np.argwhere((first != self._first) & (first == r + 1))   # receipt round r + 1
         self._first = first
         deliveries = [(self.peers[v], self.gossip_line(m)) for v, m in new.tolist()]
-        rep, _ = self.engine.reports()
+        rep, total = self.engine.reports(max(int(st["reports"]), 1))
+        if st["overflow"] or total != len(rep):
+            # a subset of the Dead Node lines would let the seed log drift from
+            # the engine's removals: the engine's report_capacity is too small
+            raise RuntimeError(f"round {r}: {total} dead-node reports, the engine kept {len(rep)} "
+                               "(raise report_capacity)")
         reports = [(self.peers[int(rp)], wire.dead_node_message(self.peers[int(d)]) + "\n")
                    for d, rp, _ in sorted(rep.tolist(), key=lambda x: (x[0], x[1]))]
         n_log = len(self.registry.logs)

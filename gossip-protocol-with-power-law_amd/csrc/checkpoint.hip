@@ -32,6 +32,8 @@ struct CkptHeader {
   int32_t liveness_active, pending_crash, msg_forwards_valid, done_dirty;
   int32_t has_first, has_frx, cmask_rows, reserved;
   uint64_t prev_next_arcs, prev_new_bits, prev_receivers, held_bits;
+  int64_t last_reports;     // reports of the round just taken (exact count)
+  int64_t saved_reports;    // how many of them the blob holds (<= the report buffer)
 };
 
 static int64_t align8(int64_t b) { return (b + 7) & ~(int64_t)7; }
@@ -64,10 +66,14 @@ static std::vector<Section> plain_sections(Ctx* c) {
   return s;
 }
 
-static int64_t blob_bytes(Ctx* c) {
+// reports of the last round held in the device buffer (gp_reports reads them
+// after a restore exactly as after the round itself)
+static int64_t saved_reports(const Ctx* c) { return std::min(c->last_reports, c->report_cap); }
+
+static int64_t blob_bytes(Ctx* c, int64_t nrep) {
   int64_t b = align8((int64_t)sizeof(CkptHeader)) + c->n_alloc * c->words * 8;   // canonical rows
   for (const Section& s : plain_sections(c)) b += align8(s.bytes);
-  return b;
+  return b + align8(nrep * (int64_t)sizeof(gp_report));
 }
 
 // rows[t] = word t % W of vertex v0 + t / W's Message-List row (zero if none)
@@ -98,14 +104,16 @@ extern "C" {
 int gp_checkpoint_size(gp_ctx* c, int64_t* bytes) {
   if (!c || !bytes) return set_error(GP_EINVAL, "null argument");
   if (!run_state(c)) return set_error(GP_ESTATE, "no run state (gp_reset first)");
-  *bytes = blob_bytes(c);
+  *bytes = blob_bytes(c, saved_reports(c));
   return 0;
 }
 
 int gp_checkpoint_save(gp_ctx* c, void* host, int64_t bytes) {
   if (!c || !host) return set_error(GP_EINVAL, "null argument");
   if (!run_state(c)) return set_error(GP_ESTATE, "no run state (gp_reset first)");
-  if (bytes != blob_bytes(c)) return set_error(GP_EINVAL, "bytes mismatch: expected " + std::to_string(blob_bytes(c)));
+  const int64_t nrep = saved_reports(c);
+  if (bytes != blob_bytes(c, nrep))
+    return set_error(GP_EINVAL, "bytes mismatch: expected " + std::to_string(blob_bytes(c, nrep)));
   GP_HIP(hipSetDevice(c->device));
   GP_HIP(hipStreamSynchronize(c->stream));
   uint8_t* out = static_cast<uint8_t*>(host);
@@ -123,6 +131,8 @@ int gp_checkpoint_save(gp_ctx* c, void* host, int64_t bytes) {
   h.cmask_rows = c->cmask_rows;
   h.prev_next_arcs = c->prev_next_arcs; h.prev_new_bits = c->prev_new_bits;
   h.prev_receivers = c->prev_receivers; h.held_bits = c->held_bits;
+  h.last_reports = c->last_reports;
+  h.saved_reports = nrep;
   std::memcpy(out, &h, sizeof(h));
   int64_t off = align8((int64_t)sizeof(CkptHeader));
   // canonical rows, staged through a device buffer
@@ -145,6 +155,7 @@ int gp_checkpoint_save(gp_ctx* c, void* host, int64_t bytes) {
     GP_TRY(copy_sync(c, out + off, s.dev, (size_t)s.bytes, hipMemcpyDeviceToHost));
     off += align8(s.bytes);
   }
+  GP_TRY(copy_sync(c, out + off, c->d_reports, (size_t)nrep * sizeof(gp_report), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -155,16 +166,25 @@ int gp_checkpoint_load(gp_ctx* c, const void* host, int64_t bytes) {
   std::memcpy(&h, host, sizeof(h));
   if (h.magic != CKPT_MAGIC) return set_error(GP_EINVAL, "not a gossip checkpoint");
   if (h.abi != GP_ABI_VERSION) return set_error(GP_EINVAL, "checkpoint of ABI " + std::to_string(h.abi));
-  // same overlay, messages, partition and tracked outputs
+  // Everything is checked against what the context knows BEFORE gp_reset, so
+  // a rejected blob leaves the run in progress untouched: same overlay,
+  // messages, partition, tracked outputs, component targets and size.
   if (h.n != c->n || h.nnz != c->nnz || h.m != c->m || h.words != c->words || h.msg_word_base != c->cfg.msg_word_base)
     return set_error(GP_EINVAL, "checkpoint of another overlay or message set");
-  GP_TRY(gp_reset(c));   // allocates the run state and the component targets
   if (h.n_alloc != c->n_alloc || h.vbegin != c->vbegin || h.vend != c->vend)
     return set_error(GP_EINVAL, "checkpoint of another partition");
-  if (h.has_first != (c->d_first && c->cfg.track_first ? 1 : 0) || h.has_frx != (c->d_frx[0] ? 1 : 0) ||
-      h.cmask_rows != c->cmask_rows)
+  if (h.has_first != (c->cfg.track_first ? 1 : 0) || h.has_frx != (c->cfg.track_msg_forwards ? 1 : 0))
     return set_error(GP_EINVAL, "checkpoint tracks other outputs (track_first / track_msg_forwards)");
-  if (bytes != blob_bytes(c)) return set_error(GP_EINVAL, "bytes mismatch: expected " + std::to_string(blob_bytes(c)));
+  GP_HIP(hipSetDevice(c->device));
+  // the component targets (cmask rows) of this message set; computing them
+  // touches no run state that could be in progress (set_messages invalidated it)
+  if (!c->d_sp || !c->d_slot[0] || !c->done_at_valid) GP_TRY(gp_reset(c));
+  if (h.cmask_rows != c->cmask_rows) return set_error(GP_EINVAL, "checkpoint of another message set (targets)");
+  if (h.saved_reports < 0 || h.saved_reports > h.last_reports || h.saved_reports > c->report_cap)
+    return set_error(GP_EINVAL, "checkpoint holds more reports than report_capacity");
+  if (bytes != blob_bytes(c, h.saved_reports))
+    return set_error(GP_EINVAL, "bytes mismatch: expected " + std::to_string(blob_bytes(c, h.saved_reports)));
+  GP_TRY(gp_reset(c));   // accepted: clear the run state, then fill it from the blob
   GP_HIP(hipSetDevice(c->device));
   const uint8_t* in = static_cast<const uint8_t*>(host);
   c->round = h.round;
@@ -190,6 +210,7 @@ int gp_checkpoint_load(gp_ctx* c, const void* host, int64_t bytes) {
     GP_TRY(copy_sync(c, s.dev, in + off, (size_t)s.bytes, hipMemcpyHostToDevice));
     off += align8(s.bytes);
   }
+  GP_TRY(copy_sync(c, c->d_reports, in + off, (size_t)h.saved_reports * sizeof(gp_report), hipMemcpyHostToDevice));
   // slot bytes: saved rows now live in S[cur]; the other slot reads as unwritten
   {
     const size_t na = (size_t)c->n_alloc;
@@ -213,7 +234,7 @@ int gp_checkpoint_load(gp_ctx* c, const void* host, int64_t bytes) {
   c->held_bits = h.held_bits;
   c->cml_written_prev = false;   // compact lists are rebuilt by the next sparse round
   c->cml_read_now = c->cml_write_now = false;
-  c->last_reports = 0;
+  c->last_reports = h.last_reports;
   return 0;
 }
 

@@ -373,11 +373,14 @@ def test_checkpoint_restore_continues_exactly(pkg, oracle, mode, stop, p_fail, t
     a = _engine(pkg, g, origin, inject, **cfg)
     for _ in range(stop):
         a.round()
-    path = tmp_path / "ck.npz"
+    saved_reports = sorted(map(tuple, a.reports()[0].tolist()))
+    path = tmp_path / "ck.npy"
     a.save_checkpoint(path)
     check(a, *tail(a))
     b = _engine(pkg, g, origin, inject, **cfg)
     b.load_checkpoint(path)
+    # the reports of the round the checkpoint was taken after come back too
+    assert sorted(map(tuple, b.reports()[0].tolist())) == saved_reports
     check(b, *tail(b))
     b.close()
     a.load_checkpoint(path)
@@ -503,3 +506,51 @@ def test_summary_probes(pkg, oracle, prefilter, churn):
     # the summary path runs in filtered pull rounds with <= n/256 senders
     assert any(s["mode"] == 0 and s["scan"] != 2 and s["active"] * 256 <= g.n for s in r["stats"])
     r["eng"].close()
+
+
+def test_checkpoint_rejected_blob_leaves_run_intact(pkg, oracle, tmp_path):
+    """A blob of another configuration (tracked outputs, partition, message
+    set) is rejected before anything is reset: the run in progress continues
+    exactly as if the load had never been tried."""
+    rp, col = oracle.chung_lu(20_000, 8, 2.4, 41)
+    g = pkg.CSR(20_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 512, seed=41)
+    inject = (np.arange(512) % 3).astype(np.int32)
+    kw = dict(churn=True, p_fail=0.02, churn_seed=4)
+    cfg = dict(track_first=1, track_digest=1, track_msg_forwards=1, churn=1, p_fail=0.02, churn_seed=4)
+    ref = oracle.run(g, origin, inject, want_first=True, **kw)
+    other = []
+    e = _engine(pkg, g, origin, inject, **dict(cfg, track_first=0))   # other tracked outputs
+    e.round()
+    other.append(e.checkpoint())
+    e.close()
+    e = _engine(pkg, g, origin[:300], inject[:300], **cfg)             # other message set
+    e.round()
+    other.append(e.checkpoint())
+    e.close()
+    e = pkg.GossipEngine(0, **cfg)                                      # other partition
+    e.load_graph(g)
+    e.set_partition(1, 2)
+    e.set_messages(origin, inject)
+    e.reset()
+    other.append(e.checkpoint())
+    e.close()
+    a = _engine(pkg, g, origin, inject, **cfg)
+    stats = [a.round(), a.round()]
+    for blob in other + [np.zeros(64, np.uint8)]:
+        with pytest.raises(pkg.GossipError):
+            a.restore(blob)
+    while True:
+        st = a.round()
+        stats.append(st)
+        if st["new_bits"] == 0 and st["round"] >= 2:
+            break
+    assert len(stats) == ref["rounds"]
+    for x, y in zip(stats, ref["stats"]):
+        for k in STAT_KEYS:
+            assert x[k] == y[k], (k, x["round"])
+    a.finalize()
+    assert np.array_equal(a.first(), ref["first"])
+    assert np.array_equal(a.digest(), ref["digest"])
+    assert np.array_equal(a.forwards(), ref["forwards"])
+    a.close()
