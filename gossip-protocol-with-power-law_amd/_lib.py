@@ -23,7 +23,7 @@ class GossipError(RuntimeError):
 GP_OK, GP_EINVAL, GP_EHIP, GP_ENOMEM, GP_ESTATE, GP_ERCCL, GP_ENOTRACK = 0, -1, -2, -3, -4, -5, -6
 
 # gp_what
-SEEN, FIRST, DIGEST, COVERAGE, FORWARDS, STATE, MISS, DEG_LIVE, ROW_PTR, COL, FRONTIER, FPOP = range(12)
+SEEN, FIRST, DIGEST, COVERAGE, FORWARDS, STATE, MISS, DEG_LIVE, ROW_PTR, COL, FRONTIER, FPOP, L2G = range(13)
 
 
 class RoundStats(ctypes.Structure):
@@ -54,6 +54,8 @@ class RoundStats(ctypes.Structure):
         ("exchange_ms", ctypes.c_double),
         ("round_ms", ctypes.c_double),
         ("kernel_ms", ctypes.c_double),
+        ("xchg_rows", ctypes.c_uint64),
+        ("xchg_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -116,12 +118,13 @@ SIGNATURES = {
     "gp_reports": (ctypes.c_int, [_P, ctypes.POINTER(Report), _I64, _PI64]),
     "gp_synchronize": (ctypes.c_int, [_P]),
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
+    "gp_local_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI64, _PI64, _PI64]),
     "gp_checkpoint_size": (ctypes.c_int, [_P, _PI64]),
     "gp_checkpoint_save": (ctypes.c_int, [_P, _P, _I64]),
     "gp_checkpoint_load": (ctypes.c_int, [_P, _P, _I64]),
 }
 
-ABI_VERSION = 11   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 12   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

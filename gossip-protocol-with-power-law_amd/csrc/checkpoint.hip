@@ -62,7 +62,7 @@ static std::vector<Section> plain_sections(Ctx* c) {
       {c->d_cmask, (int64_t)c->cmask_rows * W * 8},
   };
   if (c->d_first && c->cfg.track_first) s.push_back({c->d_first, nl * W * 64});
-  if (c->d_frx[0]) s.push_back({c->d_frx[c->cur], na * W * 8});
+  if (c->d_frx[0]) s.push_back({c->d_frx[c->cur], c->frx_rows * W * 8});
   return s;
 }
 
@@ -173,7 +173,7 @@ int gp_checkpoint_load(gp_ctx* c, const void* host, int64_t bytes) {
     return set_error(GP_EINVAL, "checkpoint of another overlay or message set");
   if (h.n_alloc != c->n_alloc || h.vbegin != c->vbegin || h.vend != c->vend)
     return set_error(GP_EINVAL, "checkpoint of another partition");
-  if (h.has_first != (c->cfg.track_first ? 1 : 0) || h.has_frx != (c->cfg.track_msg_forwards ? 1 : 0))
+  if (h.has_first != (c->cfg.track_first ? 1 : 0) || h.has_frx != (c->cfg.track_msg_forwards || c->local ? 1 : 0))
     return set_error(GP_EINVAL, "checkpoint tracks other outputs (track_first / track_msg_forwards)");
   GP_HIP(hipSetDevice(c->device));
   // the component targets (cmask rows) of this message set; computing them

@@ -188,8 +188,10 @@ struct ExpandArgs {
   u64* __restrict__ cml_next;
   const uint32_t* __restrict__ done_at;// |messages of v's component|: seenpop == done_at -> done
   uint32_t* __restrict__ fpop_next;
-  u64* __restrict__ frx;               // exact frontier rows of round r (track_msg_forwards only)
+  u64* __restrict__ frx;               // exact frontier rows of round r (track_msg_forwards, partitioned)
   u64* __restrict__ frx_next;          // exact frontier rows of round r + 1 (idem)
+  int64_t frx_rows;                    // frx covers vertices [0, frx_rows) (partitioned: the owned
+                                       // ones; a ghost's slot row IS its frontier)
   uint32_t* __restrict__ seenpop;
   uint8_t* __restrict__ first;         // may be null
   u64* __restrict__ digest;            // may be null
@@ -1421,7 +1423,7 @@ template <int W>
 __device__ __forceinline__ int stage_row(const ExpandArgs& a, int32_t u, u64* __restrict__ srow,
                                          int8_t* __restrict__ swords, int lane) {
   u64 x = 0;
-  if (lane < W) x = a.frx ? a.frx[(size_t)u * W + lane] : a.rows[(size_t)u * W + lane];
+  if (lane < W) x = (a.frx && u < a.frx_rows) ? a.frx[(size_t)u * W + lane] : a.rows[(size_t)u * W + lane];
   const u64 nzm = __ballot(x != 0ull);
   if (lane < W) srow[lane] = x;
   if (x) swords[lane_rank(nzm)] = (int8_t)lane;
@@ -1706,7 +1708,8 @@ struct InjectArgs {
   uint8_t* __restrict__ sp;
   uint8_t* __restrict__ ws;
   uint32_t* __restrict__ fpop;
-  u64* __restrict__ frx;               // exact frontier rows (track_msg_forwards only)
+  u64* __restrict__ frx;               // exact frontier rows (track_msg_forwards, partitioned)
+  int64_t frx_rows;                    // ... of vertices [0, frx_rows)
   u64* __restrict__ cmk;               // compact-list masks of slot r & 1 (or null)
   u64* __restrict__ alive;             // [W] alive messages of round r (or null)
   uint32_t* __restrict__ seenpop;
@@ -1715,7 +1718,7 @@ struct InjectArgs {
   const uint8_t* __restrict__ state;
   u64* __restrict__ partial;
   int64_t off, groups;
-  int64_t vbegin, vend;
+  int64_t vbegin, vend;                // owned local ids [vbegin, vend); beyond: ghosts / extras
   int32_t words;
   int32_t wbase;                       // global word index of local word 0 (message shards)
   int32_t r;
@@ -1727,25 +1730,29 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
   WaveStats st;
   ws_zero(st);
   const int64_t k = (int64_t)blockIdx.x * WAVES + wib;
-  if (k < a.groups) {
+  if (k < a.groups && a.origin[a.off + k] >= 0) {   // (partitioned: every origin is local, never < 0)
     const int64_t gi = a.off + k;
     const int o = a.origin[gi];
     const bool owned = o >= a.vbegin && o < a.vend;
+    // partitioned contexts hold every origin; a ghost's row in
+    // slot r & 1 is its frontier, valid while its fpop is nonzero
+    const bool ghost = o >= a.vend;
     if (a.state[o] & ST_DOWN) {
       if (owned) st.add(S_LOST, a.cnt[gi]);
     } else {
       const uint32_t cur = a.sp[o];
       const uint32_t fp = a.fpop[o];
+      const bool has_frx = a.frx && o < a.frx_rows;
       u64 b = 0, s = 0, f = 0;
       if (lane < a.words) {
         b = a.bits[gi * a.words + lane];
-        if (cur != SLOT_NONE) s = a.slot[cur][(size_t)o * a.words + lane];
-        if (a.frx && fp) f = a.frx[(size_t)o * a.words + lane];
+        if (ghost ? fp != 0u : cur != SLOT_NONE) s = a.slot[ghost ? a.rslot : cur][(size_t)o * a.words + lane];
+        if (has_frx && fp) f = a.frx[(size_t)o * a.words + lane];
       }
       __builtin_amdgcn_wave_barrier();   // the old rows are read before they are rewritten
       if (lane < a.words) {
         a.slot[a.rslot][(size_t)o * a.words + lane] = s | b;
-        if (a.frx) a.frx[(size_t)o * a.words + lane] = f | b;
+        if (has_frx) a.frx[(size_t)o * a.words + lane] = f | b;
       }
       if (a.cmk && lane == 0) a.cmk[o] = CML_DENSE;   // a sender this round, read as a full row
       if (a.alive && b) atomicOr(a.alive + lane, b);   // injected messages are forwarded this round
@@ -1788,7 +1795,8 @@ struct LiveArgs {
   gp_report* __restrict__ reports;
   u64* __restrict__ stats;           // direct counters (cursor, cand)
   u64* __restrict__ partial;
-  int64_t n, vbegin, vend;
+  const int32_t* __restrict__ l2g;   // global id of a local vertex (partitioned; null: identity)
+  int64_t n, vbegin, vend;           // local vertex slots, owned local range
   int64_t report_cap;
   u64 crash_key;
   u64 p_thresh;                      // crash iff draw < p_thresh
@@ -1833,11 +1841,12 @@ __global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t v = v0 + q;
-        uint8_t s = (uint8_t)(sw >> (8 * q));
+        uint8_t s = (uint8_t)(sw >> (8 * q)) & (uint8_t)~ST_RMNEW;   // last round's removal flag is sent
         if (v < a.n && !(s & ST_DOWN)) {
           bool crash = (s & ST_PENDING) != 0;
+          // draws by global id: every rank holding v takes the same decision
           if (!crash && (a.p_always || a.p_thresh))
-            crash = a.p_always || draw(a.crash_key, (u64)v) < a.p_thresh;
+            crash = a.p_always || draw(a.crash_key, (u64)(a.l2g ? a.l2g[v] : (int32_t)v)) < a.p_thresh;
           if (crash) {
             s = (uint8_t)((s | ST_CRASHED) & ~ST_PENDING);
             a.fpop[v] = 0;   // crash-stop: its frontier is never sent
@@ -1953,7 +1962,11 @@ __global__ __launch_bounds__(BLOCK) void k_detect(LiveArgs a) {
       const uint32_t tot = (uint32_t)__shfl((int)tot_me, c);
       if (tot == 0) continue;
       const int v = __shfl(vme, c);
-      if (lane == 0) a.state[v] |= ST_REMOVED;
+      const bool own = v >= a.vbegin && v < a.vend;
+      // (partitioned: a ghost is removed here when an owned neighbour is live --
+      // then its owner removes it too; otherwise the owner's flag comes with the
+      // boundary exchange, partition.hip)
+      if (lane == 0) a.state[v] |= (uint8_t)(ST_REMOVED | (own ? ST_RMNEW : 0));
       const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
       for (int64_t j = b + lane; j < e; j += 64) atomicSub(&a.deg_live[a.col[j]], 1);
       if (!(v >= a.vbegin && v < a.vend)) continue;
@@ -1977,7 +1990,8 @@ __global__ __launch_bounds__(BLOCK) void k_detect(LiveArgs a) {
           const u64 m = __ballot(rep);
           if (rep) {
             const u64 slot = slot0 + (u64)lane_rank(m);
-            if ((int64_t)slot < a.report_cap) a.reports[slot] = gp_report{v, u, a.r};
+            if ((int64_t)slot < a.report_cap)
+              a.reports[slot] = a.l2g ? gp_report{a.l2g[v], a.l2g[u], a.r} : gp_report{v, u, a.r};
           }
           slot0 += (u64)__popcll(m);
         }
@@ -2075,11 +2089,12 @@ static int grid_for(int64_t work, int64_t per_block) {
   return (int)g;
 }
 
-// alive sets need every receiver of the round in this context: single-rank
-// contexts (one GPU, message shards); off for vertex partitions.  Only with
-// liveness: without crashes a message stops only once its whole component
-// holds it, so F_r never narrows cm & ~seen and the bookkeeping is pure cost
-static bool alive_on(const Ctx* c) { return c->nranks == 1 && c->d_alive != nullptr && c->liveness_active; }
+// alive sets: F_{r+1} is the OR of every receiver's new row, so partitioned
+// contexts OR-reduce their partial sets in the boundary exchange
+// (partition.hip).  Only with liveness: without crashes a message stops only
+// once its whole component holds it, so F_r never narrows cm & ~seen and the
+// bookkeeping is pure cost
+static bool alive_on(const Ctx* c) { return c->d_alive != nullptr && c->liveness_active; }
 
 static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.alive = alive_on(c) ? c->d_alive + (size_t)c->cur * c->words : nullptr;
@@ -2102,6 +2117,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.cml_next = c->cml_write_now ? c->d_cml[c->cur ^ 1] : nullptr;
   a.frx = c->d_frx[0] ? c->d_frx[c->cur] : nullptr;
   a.frx_next = c->d_frx[0] ? c->d_frx[c->cur ^ 1] : nullptr;
+  a.frx_rows = c->frx_rows;
   a.done_at = c->d_done_at;
   a.gcol = c->d_gcol;
   a.midx = c->d_midx;
@@ -2119,7 +2135,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.hub_item_ptr = c->d_hub_item_ptr;
   a.hub_partial = c->d_hub_partial;
   a.hub_pnz = c->d_hub_pnz;
-  a.vbegin = c->vbegin;
+  a.vbegin = 0;   // kernels address local ids: owned vertices are [0, nloc)
   a.nloc = c->nloc();
   a.m_total = c->m;
   a.wbase = c->cfg.msg_word_base;
@@ -2171,11 +2187,11 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   const bool flat = W <= 32 && (W <= c->cfg.flat_max_words || flat_nd);
   const bool masked = !a.unfiltered && !flat && c->arc_mask_now;
   if (masked) {   // mask words of the owned vertices' in-arcs
-    const int64_t kb = c->h_row_ptr[(size_t)c->vbegin] >> 6;
-    const int64_t ke = (c->h_row_ptr[(size_t)c->vend] + 63) >> 6;
+    const int64_t kb = c->h_row_ptr[0] >> 6;
+    const int64_t ke = (c->h_row_ptr[(size_t)c->nloc()] + 63) >> 6;
     if (ke > kb)
       hipLaunchKernelGGL(k_arcmask, dim3(grid_for(ke - kb, (int64_t)WAVES * AM_WORDS)), dim3(BLOCK), 0, c->stream,
-                         c->d_gcol, c->d_abits, c->d_amask, kb, c->nnz);
+                         c->d_gcol, c->d_abits, c->d_amask, kb, c->nnz_l);
   }
   const int mode = a.unfiltered ? SCAN_UNFILTERED : SCAN_FILTERED;
   (void)hipEventRecord(c->ev[4], c->stream);
@@ -2258,7 +2274,7 @@ static int launch_expand(Ctx* c) {
   const double est = (double)((r == 0 ? 0ull : c->prev_next_arcs) + inj);
   c->mode_push = c->cfg.push_ratio > 0.0 && est * c->cfg.push_ratio <= (double)c->nnz;
   if (c->mode_push && c->nloc() > 0)
-    GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1] + c->vbegin, 0, (size_t)c->nloc() * 4, c->stream));
+    GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1], 0, (size_t)c->nloc() * 4, c->stream));
   // unfiltered pull when (nearly) every vertex is a sender: last round's
   // receivers + this round's injected origins >= unfiltered_pct % of n.  Not
   // with liveness: a crashed vertex's Message-List may hold bits it never sent.
@@ -2346,12 +2362,12 @@ static int launch_bitsum(Ctx* c, BitsumArgs a, bool cnt, bool sum) {
   return 0;
 }
 
-static int build_hubs(Ctx* c) {
+int build_hubs(Ctx* c) {
   c->h_hub_items.clear();
   std::vector<int32_t> hubs, ptr;
   const int64_t thr = c->cfg.hub_threshold;
   if (!c->h_row_ptr.empty()) {
-    for (int64_t v = c->vbegin; v < c->vend; ++v) {
+    for (int64_t v = 0; v < c->nloc(); ++v) {   // owned local ids
       const int64_t b = c->h_row_ptr[v], e = c->h_row_ptr[v + 1];
       if (e - b <= thr) continue;
       ptr.push_back((int32_t)c->h_hub_items.size());
@@ -2377,14 +2393,29 @@ static int build_hubs(Ctx* c) {
   return 0;
 }
 
+static void free_state(Ctx* c);
+
+// nranks == 1: the whole overlay, local ids = global ids.  nranks > 1: the
+// context keeps its owned slice plus ghosts (partition.hip: localize), once
+// per overlay -- the global CSR is dropped afterwards.
 static int set_partition(Ctx* c, int32_t rank, int32_t nranks) {
   if (nranks < 1 || rank < 0 || rank >= nranks) return set_error(GP_EINVAL, "bad rank/nranks");
+  if (c->local && (rank != c->rank || nranks != c->nranks))
+    return set_error(GP_ESTATE, "a partitioned context keeps its partition: reload the overlay to change it");
+  if (c->local) return 0;
+  if (nranks > 1 && c->directed)
+    return set_error(GP_EINVAL, "vertex partitions need an undirected overlay (ghost rows are in-neighbours)");
   c->rank = rank;
   c->nranks = nranks;
   c->slice = (c->n + nranks - 1) / nranks;
   c->vbegin = std::min(c->n, (int64_t)rank * c->slice);
   c->vend = std::min(c->n, c->vbegin + c->slice);
-  c->n_alloc = c->slice * nranks;
+  c->n_alloc = c->n;
+  c->base_nv = c->n;
+  if (nranks > 1) {   // local ids from here on: the message table must be set again
+    free_state(c);
+    GP_TRY(localize(c));
+  }
   return build_hubs(c);
 }
 
@@ -2404,10 +2435,14 @@ static void free_state(Ctx* c) {
   c->d_msg_fwd = nullptr;
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
   c->inject.clear();
+  c->m = 0;
+  c->words = 0;
 }
 
 int finish_graph(Ctx* c) {
   free_state(c);
+  free_partition(c);   // a new overlay: partition again from the global CSR
+  c->nnz_l = c->nnz;
   GP_TRY(dalloc(&c->d_deg_out, (size_t)c->n));
   const int64_t* rp = c->directed ? c->d_out_row_ptr : c->d_row_ptr;
   hipLaunchKernelGGL(k_degree, dim3(grid_for(c->n, 256)), dim3(256), 0, c->stream, rp, c->d_deg_out, c->n);
@@ -2428,7 +2463,10 @@ int finish_graph(Ctx* c) {
   GP_HIP(hipStreamSynchronize(c->stream));
   c->m = 0;
   c->words = 0;
-  return set_partition(c, c->rank, c->nranks);
+  const int32_t rank = c->rank, nranks = c->nranks;
+  c->rank = 0;
+  c->nranks = 1;
+  return set_partition(c, rank, nranks);
 }
 
 // (re)allocate per-run state for the current graph/messages/config
@@ -2436,12 +2474,15 @@ static int alloc_state(Ctx* c) {
   if (c->n <= 0) return set_error(GP_ESTATE, "no graph loaded");
   if (c->words <= 0) return set_error(GP_ESTATE, "no messages set");
   const size_t W = (size_t)c->words, na = (size_t)c->n_alloc, nl = (size_t)std::max<int64_t>(c->nloc(), 1);
+  // exact frontier rows only for per-message forwards (the pull reads whole
+  // Message-Lists) and for the boundary exchange of a vertex
+  // partition, which sends owned vertices' new bits: the owned rows only (a
+  // ghost's slot row is its frontier)
+  c->frx_rows = c->local ? c->nloc() : (c->cfg.track_msg_forwards ? c->n_alloc : 0);
   for (int k = 0; k < 2; ++k) {
     GP_TRY(dalloc(&c->d_slot[k], na * W));
     GP_TRY(dalloc(&c->d_fpop[k], na));
-    // exact frontier rows only for per-message forwards (the pull reads whole
-    // Message-Lists)
-    if (c->cfg.track_msg_forwards) GP_TRY(dalloc(&c->d_frx[k], na * W));
+    if (c->frx_rows > 0 || c->local) GP_TRY(dalloc(&c->d_frx[k], (size_t)std::max<int64_t>(c->frx_rows, 1) * W));
     else dfree(&c->d_frx[k]);
   }
   GP_TRY(dalloc(&c->d_sp, na));
@@ -2470,12 +2511,12 @@ static int alloc_state(Ctx* c) {
     dfree(&c->d_cmk[0]);
     dfree(&c->d_cmk[1]);
   }
-  GP_TRY(dalloc(&c->d_amask, (size_t)((c->nnz + 63) / 64 + 2)));
-  GP_HIP(hipMemsetAsync(c->d_amask, 0, (size_t)((c->nnz + 63) / 64 + 2) * 8, c->stream));
+  GP_TRY(dalloc(&c->d_amask, (size_t)((c->nnz_l + 63) / 64 + 2)));
+  GP_HIP(hipMemsetAsync(c->d_amask, 0, (size_t)((c->nnz_l + 63) / 64 + 2) * 8, c->stream));
   GP_TRY(dalloc(&c->d_done_at, na));
   c->done_at_valid = false;
-  GP_TRY(dalloc(&c->d_acc, na * W));
-  GP_HIP(hipMemsetAsync(c->d_acc, 0, na * W * 8, c->stream));
+  GP_TRY(dalloc(&c->d_acc, nl * W));   // push accumulators of the owned receivers
+  GP_HIP(hipMemsetAsync(c->d_acc, 0, nl * W * 8, c->stream));
   GP_TRY(dalloc(&c->d_tbits, (na + 63) / 64));
   GP_HIP(hipMemsetAsync(c->d_tbits, 0, (na + 63) / 64 * 8, c->stream));
   GP_TRY(dalloc(&c->d_touched, na));
@@ -2487,6 +2528,7 @@ static int alloc_state(Ctx* c) {
   c->report_cap = std::max<int64_t>(c->cfg.report_capacity, 1);
   GP_TRY(dalloc(&c->d_reports, (size_t)c->report_cap));
   GP_TRY(dalloc(&c->d_hub_partial, std::max<size_t>(c->h_hub_items.size(), 1) * W));
+  if (c->local) GP_TRY(alloc_exchange(c));
   GP_HIP(hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -2507,16 +2549,18 @@ static int compute_done_at(Ctx* c, int64_t groups) {
   hipStream_t s = c->stream;
   GP_HIP(hipMemsetAsync(cnt, 0, (size_t)c->n * 4, s));
   GP_HIP(hipMemsetAsync(c->d_done_at, 0, (size_t)c->n_alloc * 4, s));
+  // (labels are global vertex ids: cnt is indexed by label, the rest by local id)
   if (groups > 0)
     hipLaunchKernelGGL(k_count_origins, dim3(grid_for(groups, 256)), dim3(256), 0, s, c->d_inj_origin,
                        c->d_inj_cnt, groups, c->d_comp, cnt);
-  hipLaunchKernelGGL(k_done_at, dim3(grid_for(c->n, 256)), dim3(256), 0, s, c->d_comp, cnt, c->d_done_at, c->n);
+  hipLaunchKernelGGL(k_done_at, dim3(grid_for(c->n_alloc, 256)), dim3(256), 0, s, c->d_comp, cnt, c->d_done_at,
+                     c->n_alloc);
   GP_HIP(hipGetLastError());
   GP_HIP(hipStreamSynchronize(s));
   dfree(&cnt);
   // component message masks (host: K <= #groups components carry messages)
-  std::vector<int32_t> comp((size_t)c->n);
-  GP_TRY(copy_sync(c, comp.data(), c->d_comp, (size_t)c->n * 4, hipMemcpyDeviceToHost));
+  std::vector<int32_t> comp((size_t)c->n_alloc);
+  GP_TRY(copy_sync(c, comp.data(), c->d_comp, (size_t)c->n_alloc * 4, hipMemcpyDeviceToHost));
   std::vector<int32_t> idx_of_root((size_t)c->n, -1);
   std::vector<u64> masks;
   const size_t W = (size_t)c->words;
@@ -2540,7 +2584,8 @@ static int compute_done_at(Ctx* c, int64_t groups) {
   // on the engine stream: the stream is non-blocking, so a null-stream memset
   // could land after k_midx
   GP_HIP(hipMemsetAsync(c->d_midx, 0xFF, (size_t)c->n_alloc * 4, s));
-  hipLaunchKernelGGL(k_midx, dim3(grid_for(c->n, 256)), dim3(256), 0, s, c->d_comp, ior, c->d_midx, c->n);
+  hipLaunchKernelGGL(k_midx, dim3(grid_for(c->n_alloc, 256)), dim3(256), 0, s, c->d_comp, ior, c->d_midx,
+                     c->n_alloc);
   GP_HIP(hipGetLastError());
   // pristine targets (a run drops its lost messages from the working ones)
   c->cmask_rows = (int32_t)(masks.size() / W);
@@ -2758,7 +2803,10 @@ int gp_comm_init(gp_ctx* c, const void* uid, int32_t nranks, int32_t rank) {
     (void)ncclCommDestroy(c->comm);
     c->comm = nullptr;
   }
-  if (nranks == 1) return 0;
+  if (nranks != c->nranks || rank != c->rank)
+    return set_error(GP_EINVAL, "gp_comm_init: rank/nranks differ from the context's partition");
+  // (one rank too: its exchange is the counters' all-reduce over a real
+  // communicator, which is what a one-GPU box can test)
   ncclUniqueId id;
   std::memcpy(&id, uid, sizeof(id));
   GP_RCCL(ncclCommInitRank(&c->comm, nranks, id, rank));
@@ -2807,12 +2855,17 @@ int gp_set_messages(gp_ctx* c, int32_t m, const int32_t* origin, const int32_t* 
     span.cnt++;
   }
   c->inj_arcs.assign((size_t)std::max(last + 1, 0), 0);
-  for (auto& kv : c->inject)
+  for (auto& kv : c->inject)   // (global out-degrees: every rank takes the same direction)
     for (int64_t g = kv.second.off; g < kv.second.off + kv.second.cnt; ++g)
       c->inj_arcs[(size_t)kv.first] += c->h_deg_out[(size_t)g_origin[(size_t)g]];
+  const int64_t nv_before = c->n_alloc;
+  if (c->local) {   // every origin becomes a local vertex (partition.hip), then local ids
+    GP_TRY(set_extras(c, g_origin));
+    for (auto& o : g_origin) o = (int32_t)c->to_local(o);
+  }
   c->m = m;
   c->last_inject_round = last;
-  const bool realloc = words != c->words;
+  const bool realloc = words != c->words || c->n_alloc != nv_before;
   c->words = words;
   GP_TRY(dalloc(&c->d_inj_origin, g_origin.size()));
   GP_TRY(dalloc(&c->d_inj_bits, g_bits.size()));
@@ -2862,7 +2915,7 @@ int gp_reset(gp_ctx* c) {
   c->cml_read_now = c->cml_write_now = false;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
-  GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToDevice, s));
+  GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n_alloc * 4, hipMemcpyDeviceToDevice, s));
   GP_HIP(hipMemsetAsync(c->d_msg_cov, 0, W * 64 * 4 * 8, s));
   GP_HIP(hipMemsetAsync(c->d_alive, 0, 2 * W * 8, s));
   GP_HIP(hipMemsetAsync(c->d_stats, 0, (64 + (size_t)NPART * NST) * 8, s));
@@ -2880,14 +2933,18 @@ int gp_crash(gp_ctx* c, int32_t nverts, const int32_t* verts) {
   if (!c || (nverts > 0 && !verts)) return set_error(GP_EINVAL, "null argument");
   if (!state_ready(c)) return set_error(GP_ESTATE, "gp_reset first");
   GP_HIP(hipSetDevice(c->device));
-  std::vector<uint8_t> st((size_t)c->n);
-  GP_HIP(hipStreamSynchronize(c->stream));
-  GP_TRY(copy_sync(c, st.data(), c->d_state, (size_t)c->n, hipMemcpyDeviceToHost));
-  for (int32_t k = 0; k < nverts; ++k) {
+  for (int32_t k = 0; k < nverts; ++k)
     if (verts[k] < 0 || verts[k] >= c->n) return set_error(GP_EINVAL, "vertex out of range");
-    if (!(st[verts[k]] & ST_DOWN)) st[verts[k]] |= ST_PENDING;
+  // global ids; a partitioned context applies the crashes of the vertices it
+  // holds (owned, ghosts, origins) -- the others never touch its slice
+  std::vector<uint8_t> st((size_t)c->n_alloc);
+  GP_HIP(hipStreamSynchronize(c->stream));
+  GP_TRY(copy_sync(c, st.data(), c->d_state, (size_t)c->n_alloc, hipMemcpyDeviceToHost));
+  for (int32_t k = 0; k < nverts; ++k) {
+    const int64_t v = c->to_local(verts[k]);
+    if (v >= 0 && !(st[(size_t)v] & ST_DOWN)) st[(size_t)v] |= ST_PENDING;
   }
-  GP_TRY(copy_sync(c, c->d_state, st.data(), (size_t)c->n, hipMemcpyHostToDevice));
+  GP_TRY(copy_sync(c, c->d_state, st.data(), (size_t)c->n_alloc, hipMemcpyHostToDevice));
   if (nverts > 0) {
     c->liveness_active = true;
     c->pending_crash = true;
@@ -2925,9 +2982,10 @@ static int round_launch(Ctx* c) {
     la.reports = c->d_reports;
     la.stats = stats;
     la.partial = partial;
-    la.n = c->n;
-    la.vbegin = c->vbegin;
-    la.vend = c->vend;
+    la.l2g = c->local ? c->d_l2g : nullptr;
+    la.n = c->n_alloc;
+    la.vbegin = 0;
+    la.vend = c->nloc();
     la.report_cap = c->report_cap;
     la.crash_key = stream_key(c->cfg.churn_seed, STREAM_CRASH + (uint64_t)r);
     const double p = c->cfg.churn ? c->cfg.p_fail : 0.0;
@@ -2935,7 +2993,7 @@ static int round_launch(Ctx* c) {
     la.p_thresh = (p > 0.0 && p < 1.0) ? (uint64_t)std::ldexp(p, 64) : 0ull;
     la.miss_thr = c->cfg.miss_threshold;
     la.r = r;
-    hipLaunchKernelGGL(k_churn, dim3(std::min(grid_for(c->n, BLOCK), c->cu_count * 8)), dim3(BLOCK), 0, s, la);
+    hipLaunchKernelGGL(k_churn, dim3(std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8)), dim3(BLOCK), 0, s, la);
     hipLaunchKernelGGL(k_detect, dim3(c->cu_count * GP_DETECT_BLOCKS_PER_CU), dim3(BLOCK), 0, s, la);
     GP_HIP(hipGetLastError());
     c->pending_crash = false;
@@ -2954,6 +3012,7 @@ static int round_launch(Ctx* c) {
     ia.ws = c->d_ws;
     ia.fpop = c->d_fpop[c->cur];
     ia.frx = c->d_frx[0] ? c->d_frx[c->cur] : nullptr;
+    ia.frx_rows = c->frx_rows;
     ia.cmk = c->d_cmk[0] ? c->d_cmk[c->cur] : nullptr;
     ia.alive = alive_on(c) ? c->d_alive + (size_t)c->cur * c->words : nullptr;
     ia.seenpop = c->d_seenpop;
@@ -2963,8 +3022,8 @@ static int round_launch(Ctx* c) {
     ia.partial = partial;
     ia.off = it->second.off;
     ia.groups = it->second.cnt;
-    ia.vbegin = c->vbegin;
-    ia.vend = c->vend;
+    ia.vbegin = 0;
+    ia.vend = c->nloc();
     ia.words = c->words;
     ia.wbase = c->cfg.msg_word_base;
     ia.r = r;
@@ -2975,8 +3034,8 @@ static int round_launch(Ctx* c) {
       hipLaunchKernelGGL(k_lost_clear, dim3(grid_for(ia.groups * c->words, 256)), dim3(256), 0, s,
                          c->d_inj_origin, c->d_inj_bits, c->d_inj_cnt, c->d_state, c->d_midx, c->d_cmask,
                          c->d_lostcnt, ia.off, ia.groups, c->words);
-      hipLaunchKernelGGL(k_done_fix, dim3(grid_for(c->n, 256)), dim3(256), 0, s, c->d_midx, c->d_lostcnt,
-                         c->d_done_at, c->n);
+      hipLaunchKernelGGL(k_done_fix, dim3(grid_for(c->n_alloc, 256)), dim3(256), 0, s, c->d_midx, c->d_lostcnt,
+                         c->d_done_at, c->n_alloc);
       GP_HIP(hipGetLastError());
       c->done_dirty = true;
     }
@@ -2984,9 +3043,9 @@ static int round_launch(Ctx* c) {
 
   if (c->cfg.track_msg_forwards) {   // sends of round r per message (owned senders)
     BitsumArgs b{};
-    b.rows = c->d_frx[c->cur] + (size_t)c->vbegin * c->words;   // exact frontier rows
-    b.guard = c->d_fpop[c->cur] + c->vbegin;
-    b.weight = c->d_deg_live + c->vbegin;
+    b.rows = c->d_frx[c->cur];   // exact frontier rows of the owned senders
+    b.guard = c->d_fpop[c->cur];
+    b.weight = c->d_deg_live;
     b.cnt = nullptr;
     b.wsum = c->d_msg_fwd;
     b.count = c->nloc();
@@ -3002,24 +3061,20 @@ static int round_launch(Ctx* c) {
   return 0;
 }
 
-// X_r over RCCL: all-gather the owned rows of the slot written this round,
-// the popcounts and slot bytes (+ exact frontier rows when kept), sum the
-// counters.  Every rank then holds identical replicas for round r + 1.
+// X_r over RCCL.  One rank: the counters' all-reduce is the whole exchange.
+// Vertex partition: the boundary exchange of partition.hip (this round's new
+// bits of the owned vertices other ranks hold as ghosts, removal flags, alive
+// sets) and the counters' all-reduce, so that every rank takes the same
+// decisions next round.
 static int round_exchange_rccl(Ctx* c) {
-  if (!c->comm) return 0;
-  hipStream_t s = c->stream;
-  const int nx = c->cur ^ 1;
-  const size_t W = (size_t)c->words, S = (size_t)c->slice, R = (size_t)c->rank;
-  GP_RCCL(ncclGroupStart());
-  GP_RCCL(ncclAllGather(c->d_slot[nx] + R * S * W, c->d_slot[nx], S * W, ncclUint64, c->comm, s));
-  if (c->d_frx[0])
-    GP_RCCL(ncclAllGather(c->d_frx[nx] + R * S * W, c->d_frx[nx], S * W, ncclUint64, c->comm, s));
-  GP_RCCL(ncclAllGather(c->d_fpop[nx] + R * S, c->d_fpop[nx], S, ncclUint32, c->comm, s));
-  GP_RCCL(ncclAllGather(c->d_sp + R * S, c->d_sp, S, ncclUint8, c->comm, s));
-  GP_RCCL(ncclAllGather(c->d_ws + R * S, c->d_ws, S, ncclUint8, c->comm, s));
+  if (!c->comm) {
+    if (c->local) return set_error(GP_ESTATE, "a partitioned context exchanges over RCCL (gp_comm_init) "
+                                              "or in gp_round_group");
+    return 0;
+  }
+  if (c->local) return exchange_rccl(c);
   // the report cursor (slot S_REPORT_CURSOR) stays rank-local
-  GP_RCCL(ncclAllReduce(c->d_stats, c->d_stats, S_REPORT_CURSOR, ncclUint64, ncclSum, c->comm, s));
-  GP_RCCL(ncclGroupEnd());
+  GP_RCCL(ncclAllReduce(c->d_stats, c->d_stats, S_REPORT_CURSOR, ncclUint64, ncclSum, c->comm, c->stream));
   return 0;
 }
 
@@ -3061,6 +3116,8 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
       out->kernel_ms = kms;
     }
     out->overflow = (int64_t)h[S_REPORT_CURSOR] > c->report_cap ? 1 : 0;
+    out->xchg_rows = h[S_XROWS];
+    out->xchg_bytes = h[S_XBYTES];
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
     out->expand_ms = ms;
@@ -3086,6 +3143,8 @@ extern "C" {
 
 int gp_round(gp_ctx* c, gp_round_stats* out) {
   if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (c->local && !c->comm)
+    return set_error(GP_ESTATE, "a partitioned context exchanges over RCCL (gp_comm_init) or in gp_round_group");
   GP_TRY(round_launch(c));
   GP_TRY(round_exchange_rccl(c));
   return round_collect(c, out);
@@ -3102,32 +3161,11 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
       return set_error(GP_EINVAL, "contexts out of step");
   }
   for (int32_t k = 0; k < nctx; ++k) GP_TRY(round_launch(ctxs[k]));
-  for (int32_t k = 0; k < nctx; ++k) {
-    GP_HIP(hipSetDevice(ctxs[k]->device));
-    GP_HIP(hipStreamSynchronize(ctxs[k]->stream));
-  }
-  // X_r by device-to-device copies: every context receives every other's slice
-  for (int32_t d = 0; d < nctx; ++d) {
-    Ctx* dst = ctxs[d];
-    GP_HIP(hipSetDevice(dst->device));
-    const int nx = dst->cur ^ 1;
-    const size_t W = (size_t)dst->words;
-    for (int32_t k = 0; k < nctx; ++k) {
-      if (k == d) continue;
-      Ctx* src = ctxs[k];
-      const int64_t b = src->vbegin, e = src->vend;
-      if (e <= b) continue;
-      const int sx = src->cur ^ 1;
-      GP_HIP(hipMemcpyAsync(dst->d_slot[nx] + (size_t)b * W, src->d_slot[sx] + (size_t)b * W,
-                            (size_t)(e - b) * W * 8, hipMemcpyDefault, dst->stream));
-      if (dst->d_frx[0] && src->d_frx[0])
-        GP_HIP(hipMemcpyAsync(dst->d_frx[nx] + (size_t)b * W, src->d_frx[sx] + (size_t)b * W,
-                              (size_t)(e - b) * W * 8, hipMemcpyDefault, dst->stream));
-      GP_HIP(hipMemcpyAsync(dst->d_fpop[nx] + b, src->d_fpop[sx] + b, (size_t)(e - b) * 4,
-                            hipMemcpyDefault, dst->stream));
-      GP_HIP(hipMemcpyAsync(dst->d_sp + b, src->d_sp + b, (size_t)(e - b), hipMemcpyDefault, dst->stream));
-      GP_HIP(hipMemcpyAsync(dst->d_ws + b, src->d_ws + b, (size_t)(e - b), hipMemcpyDefault, dst->stream));
-    }
+  // X_r: the boundary exchange through device-to-device copies -- the same
+  // pack / unpack as over RCCL (partition.hip)
+  if (nctx > 1) {
+    std::vector<Ctx*> cs(ctxs, ctxs + nctx);
+    GP_TRY(exchange_group(cs.data(), nctx));
   }
   gp_round_stats sum;
   std::vector<u64> own_held((size_t)nctx, 0);
@@ -3145,10 +3183,12 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     sum.rows_gathered += st.rows_gathered; sum.seen_rows_read += st.seen_rows_read;
     sum.rows_written += st.rows_written; sum.vertices_visited += st.vertices_visited;
     sum.atomics += st.atomics; sum.next_arcs += st.next_arcs; sum.mode = st.mode;
-    sum.row_bytes += st.row_bytes;
+    sum.row_bytes += st.row_bytes; sum.scan = st.scan;
+    sum.xchg_rows += st.xchg_rows; sum.xchg_bytes += st.xchg_bytes;
     sum.expand_ms = std::max(sum.expand_ms, st.expand_ms);
     sum.exchange_ms = std::max(sum.exchange_ms, st.exchange_ms);
     sum.round_ms = std::max(sum.round_ms, st.round_ms);
+    sum.kernel_ms = std::max(sum.kernel_ms, st.kernel_ms);
   }
   for (int32_t k = 0; k < nctx; ++k) {   // every context takes the same decisions next round
     ctxs[k]->prev_next_arcs = sum.next_arcs;
@@ -3189,10 +3229,10 @@ int gp_finalize_messages(gp_ctx* c) {
   GP_HIP(hipMemsetAsync(cov, 0, M * 8, s));
   if (fwd_from_seen) GP_HIP(hipMemsetAsync(fwd_local, 0, M * 8, s));
   BitsumArgs b{};
-  b.slot[0] = c->d_slot[0] + (size_t)c->vbegin * c->words;   // seen row i = slot[sp[i]][i]
-  b.slot[1] = c->d_slot[1] + (size_t)c->vbegin * c->words;
-  b.sel = c->d_sp + c->vbegin;
-  b.weight = c->d_deg_out + c->vbegin;
+  b.slot[0] = c->d_slot[0];   // seen row i = slot[sp[i]][i], owned local ids [0, nloc)
+  b.slot[1] = c->d_slot[1];
+  b.sel = c->d_sp;
+  b.weight = c->d_deg_out;
   b.cnt = cov;
   b.wsum = fwd_from_seen ? fwd_local : nullptr;
   b.count = c->nloc();
@@ -3214,7 +3254,9 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
   if (!c || !host) return set_error(GP_EINVAL, "null argument");
   GP_HIP(hipSetDevice(c->device));
   GP_HIP(hipStreamSynchronize(c->stream));
-  const int64_t W = c->words, nl = c->nloc(), M = c->m, n = c->n;
+  // partitioned contexts read their owned slice of the per-vertex arrays
+  // (local ids [0, nloc) = global [vbegin, vend)) and their local CSR
+  const int64_t W = c->words, nl = c->nloc(), M = c->m, n = c->local ? c->nloc() : c->n;
   auto need = [&](int64_t b) -> int {
     if (bytes != b) return set_error(GP_EINVAL, "bytes mismatch: expected " + std::to_string(b));
     return 0;
@@ -3227,10 +3269,9 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       if (bytes) {   // owned rows of both slots, picked per vertex by its slot byte
         std::vector<uint64_t> s1((size_t)(nl * W));
         std::vector<uint8_t> sp((size_t)nl);
-        const size_t off = (size_t)c->vbegin * W;
-        GP_TRY(copy_sync(c, host, c->d_slot[0] + off, (size_t)bytes, hipMemcpyDeviceToHost));
-        GP_TRY(copy_sync(c, s1.data(), c->d_slot[1] + off, (size_t)bytes, hipMemcpyDeviceToHost));
-        GP_TRY(copy_sync(c, sp.data(), c->d_sp + c->vbegin, (size_t)nl, hipMemcpyDeviceToHost));
+        GP_TRY(copy_sync(c, host, c->d_slot[0], (size_t)bytes, hipMemcpyDeviceToHost));
+        GP_TRY(copy_sync(c, s1.data(), c->d_slot[1], (size_t)bytes, hipMemcpyDeviceToHost));
+        GP_TRY(copy_sync(c, sp.data(), c->d_sp, (size_t)nl, hipMemcpyDeviceToHost));
         uint64_t* h = static_cast<uint64_t*>(host);
         for (int64_t v = 0; v < nl; ++v) {
           if (sp[(size_t)v] == SLOT_NONE) std::memset(h + v * W, 0, (size_t)W * 8);
@@ -3268,21 +3309,32 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(n));
       GP_TRY(copy_sync(c, host, what == GP_STATE ? c->d_state : c->d_miss, (size_t)n, hipMemcpyDeviceToHost));
+      if (what == GP_STATE)   // (the per-round removal flag is exchange bookkeeping)
+        for (int64_t v = 0; v < n; ++v) static_cast<uint8_t*>(host)[v] &= (uint8_t)~ST_RMNEW;
       return 0;
     case GP_DEG_LIVE:
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(n * 4));
       GP_TRY(copy_sync(c, host, c->d_deg_live, (size_t)bytes, hipMemcpyDeviceToHost));
       return 0;
-    case GP_ROW_PTR:
-      if (n <= 0) return set_error(GP_ESTATE, "no graph");
-      GP_TRY(need((n + 1) * 8));
+    case GP_ROW_PTR:   // partitioned: the local CSR over all local slots
+      if (c->n <= 0) return set_error(GP_ESTATE, "no graph");
+      GP_TRY(need((c->n_alloc + 1) * 8));
       GP_TRY(copy_sync(c, host, c->d_row_ptr, (size_t)bytes, hipMemcpyDeviceToHost));
       return 0;
     case GP_COL:
-      if (n <= 0) return set_error(GP_ESTATE, "no graph");
-      GP_TRY(need(c->nnz * 4));
+      if (c->n <= 0) return set_error(GP_ESTATE, "no graph");
+      GP_TRY(need(c->nnz_l * 4));
       if (bytes) GP_TRY(copy_sync(c, host, c->d_col, (size_t)bytes, hipMemcpyDeviceToHost));
+      return 0;
+    case GP_L2G:   // global id of every local slot
+      if (c->n <= 0) return set_error(GP_ESTATE, "no graph");
+      GP_TRY(need(c->n_alloc * 4));
+      if (c->local) {
+        GP_TRY(copy_sync(c, host, c->d_l2g, (size_t)bytes, hipMemcpyDeviceToHost));
+      } else {
+        for (int64_t v = 0; v < c->n; ++v) static_cast<int32_t*>(host)[v] = (int32_t)v;
+      }
       return 0;
 #ifdef GP_DBG_READ   // scripts/debug_mask2.py: arc mask, gather-order columns, activity bits
     case 100:
@@ -3304,7 +3356,7 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       if (!run) return set_error(GP_ESTATE, "no run state");
       // exact frontier rows exist only with track_msg_forwards: the pull reads
       // whole Message-Lists
-      if (!c->d_frx[0]) return set_error(GP_ENOTRACK, "frontier rows are kept only with track_msg_forwards");
+      if (!c->cfg.track_msg_forwards) return set_error(GP_ENOTRACK, "frontier rows are kept only with track_msg_forwards");
       GP_TRY(need(n * W * 8));
       std::vector<uint32_t> fp((size_t)n);
       GP_TRY(copy_sync(c, fp.data(), c->d_fpop[c->cur], (size_t)n * 4, hipMemcpyDeviceToHost));
@@ -3342,6 +3394,17 @@ int gp_info(gp_ctx* c, int64_t* n, int64_t* nnz, int32_t* m, int32_t* words) {
   if (nnz) *nnz = c->nnz;
   if (m) *m = c->m;
   if (words) *words = c->words;
+  return 0;
+}
+
+int gp_local_info(gp_ctx* c, int64_t* nloc, int64_t* nghost, int64_t* nextra, int64_t* nnz_local,
+                  int64_t* n_boundary) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (nloc) *nloc = c->nloc();
+  if (nghost) *nghost = c->nghost;
+  if (nextra) *nextra = c->nextra;
+  if (nnz_local) *nnz_local = c->nnz_l;
+  if (n_boundary) *n_boundary = c->n_bnd;
   return 0;
 }
 

@@ -22,7 +22,9 @@ typedef unsigned long long u64;
 enum StatSlot {
   S_INJECTED = 0, S_LOST, S_NEW_BITS, S_RECEIVERS, S_SENDS, S_ACTIVE, S_CRASHED,
   S_REPORTS, S_REMOVALS, S_DUP, S_ARCS, S_GATHERED, S_SEEN_READ, S_WRITTEN,
-  S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_ROW_BYTES, NST,
+  S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_ROW_BYTES,
+  S_XROWS, S_XBYTES,   // boundary entries / bytes sent (vertex partition, written by the pack step)
+  NST,
   S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR
 };
 
@@ -51,11 +53,52 @@ struct Ctx {
   int32_t* d_comp = nullptr;          // weakly connected component label (min vertex id)
   std::vector<int64_t> h_row_ptr;     // host copy (hub table, partition)
 
-  // partition
+  // partition.  Kernels address vertices by LOCAL id: one rank (nranks == 1)
+  // holds the whole overlay and local == global; a vertex-partitioned context
+  // (nranks > 1, partition.hip) holds its owned slice as local ids [0, nloc),
+  // then its ghosts -- the non-owned in-neighbours of owned vertices, sorted by
+  // global id, hence grouped by owner -- then the message origins that are
+  // neither ("extras", so that every rank sees every origin's liveness).
   int32_t rank = 0, nranks = 1;
-  int64_t slice = 0;                  // rows per rank (padded)
-  int64_t vbegin = 0, vend = 0;       // owned vertices
-  int64_t n_alloc = 0;                // nranks * slice
+  int64_t slice = 0;                  // owned vertices per rank (ceil(n / nranks))
+  int64_t vbegin = 0, vend = 0;       // owned vertices, GLOBAL ids
+  int64_t n_alloc = 0;                // local vertex slots: nloc + nghost + nextra
+  bool local = false;                 // vertex-partitioned (local ids != global ids)
+  int64_t nghost = 0, nextra = 0;
+  int64_t nnz_l = 0;                  // arcs of the device CSR (local CSR when partitioned)
+  int32_t* d_l2g = nullptr;           // [n_alloc] global id of each local vertex (partitioned only)
+  std::vector<int32_t> h_l2g;         // host copy
+  std::vector<int32_t> h_comp_g;      // global component labels (extras need theirs)
+  std::vector<int32_t> h_deg_g;       // global degrees (partitioned: extras, inj_arcs)
+  int64_t base_nv = 0;                // nloc + nghost (local slots before the extras)
+  // boundary exchange (partitioned): the owned vertices that are
+  // ghosts on rank q, peer-major (flat entry t, [bnd_ptr[q], bnd_ptr[q+1])) and
+  // vertex-major (owned boundary vertex k -> its entries).  Rank q's ghosts of
+  // owner p are, in the same order, exactly B_pq: no id lists are exchanged.
+  std::vector<int64_t> h_bnd_ptr;     // [nranks + 1]
+  std::vector<int64_t> h_gh_ptr;      // [nranks + 1] ghost index offsets per owner
+  int64_t n_bnd = 0, n_bvx = 0;       // flat entries, owned boundary vertices
+  int32_t* d_bnd_e = nullptr;         // [n_bnd] index of entry t within its peer list
+  int32_t* d_bnd_k = nullptr;         // [n_bnd] vertex-major index of entry t
+  int32_t* d_bvx_v = nullptr;         // [n_bvx] owned local vertex
+  int32_t* d_bvx_ptr = nullptr;       // [n_bvx + 1] -> d_bvx_t
+  int32_t* d_bvx_t = nullptr;         // [n_bnd] entries of vertex k
+  int64_t* d_bnd_ptr = nullptr;       // [nranks + 1]
+  u64* d_bvx_info = nullptr;          // [n_bvx] word mask of this round's new row (0: none)
+  uint8_t* d_bvx_flag = nullptr;      // [n_bvx] bit 0: new row, bit 1: removed this round
+  u64* d_bnd_scan = nullptr;          // [n_bnd + 1] exclusive scan of (heads << 40 | words)
+  u64* d_xsize = nullptr;             // [max(n_bnd, nghost) + 1] entry sizes (scan input)
+  u64* d_sbuf_h = nullptr;            // send heads (e | flags << 32 | popc << 40)
+  u64* d_sbuf_w = nullptr;            // send words (mask word, then the nonzero words)
+  u64* d_rbuf_h = nullptr;            // received heads, by sender rank
+  u64* d_rbuf_w = nullptr;            // received words, by sender rank
+  u64* d_rscan = nullptr;             // [nghost + 1] word offsets of the received entries
+  u64* d_cnt = nullptr;               // [4 * nranks] per peer: head start, heads, word start, words
+  u64* d_cnt_all = nullptr;           // [nranks][4 * nranks]
+  u64* h_cnt_all = nullptr;           // pinned copy
+  u64* d_alive_all = nullptr;         // [nranks][W]
+  void* d_scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
 
   // messages
   int32_t m = 0, words = 0;
@@ -73,7 +116,8 @@ struct Ctx {
   u64* d_slot[2] = {nullptr, nullptr};    // [n_alloc][W]
   uint8_t* d_sp = nullptr;          // [n_alloc] slot of v's seen row (0xFF: none)
   uint8_t* d_ws = nullptr;          // [n_alloc] bit p: slot p written this run
-  u64* d_frx[2] = {nullptr, nullptr};     // exact frontier rows (track_msg_forwards only)
+  u64* d_frx[2] = {nullptr, nullptr};     // exact frontier rows (track_msg_forwards; partitioned)
+  int64_t frx_rows = 0;                   // rows d_frx covers (partitioned: the owned ones)
   uint32_t* d_fpop[2] = {nullptr, nullptr};    // [n_alloc]
   int cur = 0;
   uint32_t* d_seenpop = nullptr;    // [nloc]
@@ -157,6 +201,8 @@ struct Ctx {
   int cu_count = 256;
 
   int64_t nloc() const { return vend - vbegin; }
+  // lookup of a global vertex id among the local ids (-1: not local)
+  int64_t to_local(int64_t g) const;
 
 };
 
@@ -204,6 +250,18 @@ int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed);
 int build_gather_order(Ctx* c);
 // gossip_engine.hip
 int finish_graph(Ctx* c);
+int build_hubs(Ctx* c);
+// partition.hip
+int localize(Ctx* c);                          // global overlay -> owned + ghost local CSR, boundary lists
+int set_extras(Ctx* c, const std::vector<int32_t>& origins_global);   // origins neither owned nor ghosts
+void free_partition(Ctx* c);
+int alloc_exchange(Ctx* c);                    // exchange buffers for the current row width
+int pack_boundary(Ctx* c);                     // after E_r: this round's boundary entries -> send buffers
+int exchange_rccl(Ctx* c);                     // counts, rows, alive sets over RCCL, then unpack
+int exchange_group(Ctx** ctxs, int32_t nctx);  // the same through device-to-device copies
+// state bit: removed by this rank's seed step in the current round (sent to the
+// ranks holding the vertex as a ghost; cleared by the next round's k_churn)
+constexpr uint8_t ST_RMNEW = 8;
 
 }  // namespace gp
 

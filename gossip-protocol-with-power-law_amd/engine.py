@@ -31,6 +31,7 @@ class GossipEngine:
         self.words = 0
         self.origin = None
         self.inject_round = None
+        self.nranks = 1
         if config:
             self.configure(**config)
 
@@ -72,7 +73,11 @@ class GossipEngine:
         self.n = int(n)
 
     def graph(self):
+        """The overlay as loaded / built (global CSR).  A partitioned context
+        keeps only its local CSR: see local_graph()."""
         from .overlay import CSR
+        if self.nranks > 1:
+            raise RuntimeError("a partitioned context holds its local CSR only (local_graph())")
         n, nnz = self.info()[:2]
         rp = np.empty(n + 1, dtype=np.int64)
         col = np.empty(nnz, dtype=np.int32)
@@ -80,9 +85,28 @@ class GossipEngine:
         check(self._lib.gp_read(self._ctx, _lib.COL, _ptr(col), col.nbytes))
         return CSR(n, rp, col, False)
 
+    def local_info(self):
+        """(nloc, nghost, nextra, nnz_local, n_boundary) of this context."""
+        v = [ctypes.c_int64() for _ in range(5)]
+        check(self._lib.gp_local_info(self._ctx, *[ctypes.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
+    def local_graph(self):
+        """(row_ptr, col, l2g) of the context's local CSR: owned vertices
+        [0, nloc) with their full in-lists, ghosts with their owned neighbours,
+        origin extras with none; l2g maps local ids to global ids."""
+        nloc, ng, nx, nnz_l, _ = self.local_info()
+        nv = nloc + ng + nx if self.nranks > 1 else self.n
+        rp = self._read(_lib.ROW_PTR, np.empty(nv + 1, dtype=np.int64))
+        col = self._read(_lib.COL, np.empty(nnz_l, dtype=np.int32))
+        l2g = self._read(_lib.L2G, np.empty(nv, dtype=np.int32))
+        return rp, col, l2g
+
     def degrees(self):
         """Degree of every vertex of the loaded overlay (in-degree of the
         in-CSR; = degree for undirected overlays), from row_ptr alone."""
+        if self.nranks > 1:
+            raise RuntimeError("degrees() needs the global overlay (check it before partitioning)")
         n = self.info()[0]
         rp = np.empty(n + 1, dtype=np.int64)
         check(self._lib.gp_read(self._ctx, _lib.ROW_PTR, _ptr(rp), rp.nbytes))
@@ -103,7 +127,13 @@ class GossipEngine:
 
     # -- partition / RCCL --------------------------------------------------
     def set_partition(self, rank, nranks):
+        """Vertex partition: keep the owned slice of rank `rank`
+        of `nranks` plus ghost rows; nranks > 1 drops the global CSR and the
+        message table (set_messages again, in global ids)."""
         check(self._lib.gp_set_partition(self._ctx, int(rank), int(nranks)))
+        self.nranks = int(nranks)
+        if nranks > 1:
+            self.m = self.words = 0
 
     def partition(self):
         b, e = ctypes.c_int64(), ctypes.c_int64()
@@ -251,17 +281,20 @@ class GossipEngine:
     def forwards(self):
         return self._read(_lib.FORWARDS, np.empty(self.m, dtype=np.uint64))
 
+    def _nv(self):   # per-vertex reads: the owned slice of a partitioned context
+        return self.nloc() if self.nranks > 1 else self.n
+
     def state(self):
-        return self._read(_lib.STATE, np.empty(self.n, dtype=np.uint8))
+        return self._read(_lib.STATE, np.empty(self._nv(), dtype=np.uint8))
 
     def miss(self):
-        return self._read(_lib.MISS, np.empty(self.n, dtype=np.uint8))
+        return self._read(_lib.MISS, np.empty(self._nv(), dtype=np.uint8))
 
     def deg_live(self):
-        return self._read(_lib.DEG_LIVE, np.empty(self.n, dtype=np.int32))
+        return self._read(_lib.DEG_LIVE, np.empty(self._nv(), dtype=np.int32))
 
     def frontier(self):
-        return self._read(_lib.FRONTIER, np.empty((self.n, self.words), dtype=np.uint64))
+        return self._read(_lib.FRONTIER, np.empty((self._nv(), self.words), dtype=np.uint64))
 
     def reports(self, cap=1 << 20):
         """Reports of the last round as int32 [k, 3] (dead, reporter, round),

@@ -24,10 +24,14 @@
  *     sets are run as independent batches by the host -- messages never interact).
  *   - Multi-GPU: one process per GPU.  Either message shards (each context
  *     runs the whole overlay for a word-aligned block of messages,
- *     gp_config.msg_word_base; no collective), or a vertex partition: each
- *     context owns a contiguous slice [vbegin, vend) of equal size and
- *     exchanges its new Message-List rows by RCCL all-gather over xGMI after
- *     every round (gp_comm_init).
+ *     gp_config.msg_word_base; no collective), or a vertex partition
+ *     (gp_set_partition, nranks > 1, undirected overlays): each context keeps
+ *     its owned slice [vbegin, vend) plus ghost rows for the non-owned
+ *     in-neighbours of owned vertices, and after every round sends each peer
+ *     only the new bits of the boundary vertices that received something
+ *     (ncclSend / ncclRecv over xGMI, gp_comm_init; or device-to-device copies
+ *     in gp_round_group).  Per-vertex reads of a partitioned context return its
+ *     owned slice; its CSR reads return the local CSR (GP_L2G maps local ids).
  */
 #ifndef GOSSIP_CAPI_H
 #define GOSSIP_CAPI_H
@@ -38,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 11
+#define GP_ABI_VERSION 12
 
 typedef struct gp_ctx gp_ctx;
 
@@ -86,6 +90,8 @@ typedef struct gp_round_stats {
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
   double kernel_ms;         /* device time of the main pull kernel k_expand alone    */
+  uint64_t xchg_rows;       /* vertex partition: boundary entries sent (all peers)   */
+  uint64_t xchg_bytes;      /* vertex partition: bytes sent (entry heads + words)    */
 } gp_round_stats;
 
 /* One dead-node report: reporter saw `dead` miss 3 heartbeats in `round`. */
@@ -144,7 +150,9 @@ typedef enum gp_what {
   GP_COL = 9,         /* i32 [nnz] in-CSR columns                                    */
   GP_FRONTIER = 10,   /* u64 [n][W] current frontier (rows with FPOP==0 read as 0);
                          kept only with track_msg_forwards (else GP_ENOTRACK)      */
-  GP_FPOP = 11        /* u32 [n] |frontier(v)|                                       */
+  GP_FPOP = 11,       /* u32 [n] |frontier(v)|                                       */
+  GP_L2G = 12         /* i32 [local slots] global id of each local vertex (identity
+                         unless partitioned: owned, then ghosts, then origin extras) */
 } gp_what;
 
 int gp_abi_version(void);
@@ -199,6 +207,10 @@ int gp_read(gp_ctx* ctx, int32_t what, void* host, int64_t bytes);
 int gp_reports(gp_ctx* ctx, gp_report* buf, int64_t cap, int64_t* n_out);
 int gp_synchronize(gp_ctx* ctx);
 int gp_info(gp_ctx* ctx, int64_t* n, int64_t* nnz, int32_t* m, int32_t* words);
+/* Local shape of a (partitioned) context: owned vertices, ghosts, origin
+ * extras, arcs of the local CSR, boundary entries it sends to (all peers). */
+int gp_local_info(gp_ctx* ctx, int64_t* nloc, int64_t* nghost, int64_t* nextra, int64_t* nnz_local,
+                  int64_t* n_boundary);
 
 /* Checkpoints (no reference counterpart -- the
  * reference's peers keep no state across restarts).  Taken between rounds:

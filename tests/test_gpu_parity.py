@@ -196,42 +196,172 @@ def test_c3_chung_lu_1e6_1024(pkg, oracle, mode):
     assert np.array_equal(fwd, ref["forwards"])
 
 
+def _group_run(pkg, g, origin, inject, P, crashes=(), **cfg):
+    """Vertex partition over P contexts on one GPU (gp_round_group: the
+    boundary exchange through device-to-device copies)."""
+    engs = []
+    for k in range(P):
+        e = pkg.GossipEngine(0, **cfg)
+        e.load_graph(g)
+        e.set_partition(k, P)
+        e.set_messages(origin, inject)
+        e.reset()
+        engs.append(e)
+    by_round = {}
+    for v, r in crashes:
+        by_round.setdefault(r, []).append(v)
+    stats, reports = [], []
+    last = int(np.max(inject)) if inject is not None and len(inject) else 0
+    for r in range(254):
+        if r in by_round:
+            for e in engs:   # the host hands every rank the same (global) crash list
+                e.crash(by_round[r])
+        st = pkg.GossipEngine.round_group(engs)
+        stats.append(st)
+        for e in engs:
+            rep, nrep = e.reports()
+            assert nrep == len(rep)
+            reports.extend(map(tuple, rep.tolist()))
+        if st["new_bits"] == 0 and r >= last:
+            break
+    return engs, stats, reports
+
+
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
-def test_group_partition_invariance(pkg, oracle, mode):
-    """2 and 3 contexts on one GPU (device-to-device exchange) == 1 context."""
+@pytest.mark.parametrize("churn", [False, True])
+def test_group_partition_invariance(pkg, oracle, mode, churn):
+    """Vertex partition over P = 2, 3, 4 contexts: owned
+    slices + ghost rows, the sparse boundary exchange of this round's new
+    bits (and removal flags) through the same pack / unpack buffers as the
+    RCCL path.  Every output equals the oracle's (one context)."""
     push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
     origin = pkg.overlay.random_origins(g.n, 200, seed=8)
     inject = (np.arange(200) % 4).astype(np.int32)
-    ref = oracle.run(g, origin, inject, churn=True, p_fail=0.02, churn_seed=3, want_first=True)
-    for P in (2, 3):
-        engs = []
-        for k in range(P):
-            e = pkg.GossipEngine(0, track_first=1, churn=1, p_fail=0.02, churn_seed=3, track_msg_forwards=1,
-                                 push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
-            e.load_graph(g)
-            e.set_partition(k, P)
-            e.set_messages(origin, inject)
-            e.reset()
-            engs.append(e)
-        stats = pkg.GossipEngine.run_group(engs)
-        assert len(stats) == ref["rounds"]
+    kw = dict(churn=True, p_fail=0.02, churn_seed=3) if churn else {}
+    crashes = [(int(origin[5]), 1), (17, 2)] if churn else []
+    ref = oracle.run(g, origin, inject, crashes=crashes, want_first=True, **kw)
+    cfg = dict(track_first=1, track_msg_forwards=int(churn), push_ratio=push_ratio, unfiltered_pct=unfiltered_pct,
+               flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
+    if churn:
+        cfg.update(churn=1, p_fail=0.02, churn_seed=3)
+    for P in (2, 3, 4):
+        engs, stats, reports = _group_run(pkg, g, origin, inject, P, crashes, **cfg)
+        assert len(stats) == ref["rounds"], P
         for a, b in zip(stats, ref["stats"]):
             for k in STAT_KEYS:
-                assert a[k] == b[k], (P, k, a["round"])
+                assert a[k] == b[k], (P, k, a["round"], a[k], b[k])
+        assert sum(s["xchg_rows"] for s in stats) > 0
+        assert sorted(reports) == sorted(map(tuple, ref["reports"].tolist()))
         first = np.concatenate([e.first() for e in engs])
         digest = np.concatenate([e.digest() for e in engs])
+        seen = np.concatenate([e.seen() for e in engs])
         assert np.array_equal(first, ref["first"])
         assert np.array_equal(digest, ref["digest"])
+        assert np.array_equal(seen, ref["seen"][:, :engs[0].words])
         cov = fwd = 0
         for e in engs:
             e.finalize()
             cov = cov + e.coverage()
-            fwd = fwd + e.forwards()
+            if churn:
+                fwd = fwd + e.forwards()
+            else:
+                fwd = fwd + e.forwards()
         assert np.array_equal(cov, ref["coverage"])
         assert np.array_equal(fwd, ref["forwards"])
+        if churn:   # owned slices of the vertex state agree with one context's
+            with pkg.GossipEngine(0, **cfg) as one:
+                one.load_graph(g)
+                one.set_messages(origin, inject)
+                one.reset()
+                by_round = {}
+                for v, r in crashes:
+                    by_round.setdefault(r, []).append(v)
+                for r in range(len(stats)):
+                    if r in by_round:
+                        one.crash(by_round[r])
+                    one.round()
+                assert np.array_equal(np.concatenate([e.state() for e in engs]), one.state())
+                assert np.array_equal(np.concatenate([e.deg_live() for e in engs]), one.deg_live())
+                assert np.array_equal(np.concatenate([e.miss() for e in engs]), one.miss())
         for e in engs:
             e.close()
+
+
+def test_partition_local_graph(pkg):
+    """The local CSR of a partition: owned rows are the global in-lists
+    (gather order, local ids), ghost rows list their owned neighbours, and
+    every rank's ghosts of owner p are exactly the vertices p sends to it."""
+    g = pkg.overlay.barabasi_albert(2000, 3, seed=1)
+    P = 3
+    origin = np.array([0, 1999, 1000], np.int32)
+    locs = []
+    for k in range(P):
+        with pkg.GossipEngine(0) as e:
+            e.load_graph(g)
+            e.set_partition(k, P)
+            e.set_messages(origin)
+            vb, ve = e.partition()
+            rp, col, l2g = e.local_graph()
+            locs.append((vb, ve, rp, col, l2g, e.local_info()))
+    S = -(-g.n // P)
+    for k, (vb, ve, rp, col, l2g, (nloc, ng, nx, nnz_l, nb)) in enumerate(locs):
+        assert (vb, ve) == (k * S, min(g.n, (k + 1) * S)) and nloc == ve - vb
+        assert np.array_equal(l2g[:nloc], np.arange(vb, ve))
+        ghosts = l2g[nloc:nloc + ng]
+        assert np.all(np.diff(ghosts) > 0) and not np.any((ghosts >= vb) & (ghosts < ve))
+        extras = l2g[nloc + ng:]
+        assert set(extras.tolist()) == {int(o) for o in origin if not (vb <= o < ve) and o not in set(ghosts.tolist())}
+        for i in range(nloc):   # owned rows: the whole in-list
+            v = vb + i
+            assert sorted(l2g[col[rp[i]:rp[i + 1]]].tolist()) == g.col[g.row_ptr[v]:g.row_ptr[v + 1]].tolist()
+        for x in range(nloc, nloc + ng):   # ghost rows: owned neighbours
+            u = int(l2g[x])
+            nb_own = [w for w in g.col[g.row_ptr[u]:g.row_ptr[u + 1]].tolist() if vb <= w < ve]
+            assert sorted(l2g[col[rp[x]:rp[x + 1]]].tolist()) == nb_own
+        assert rp[-1] == nnz_l and np.all(np.diff(rp[nloc + ng:]) == 0)
+        # boundary entries = sum over peers of the ghosts they hold from this rank
+        held = sum(int(np.sum((o[4][o[5][0]:o[5][0] + o[5][1]] >= vb) & (o[4][o[5][0]:o[5][0] + o[5][1]] < ve)))
+                   for j, o in enumerate(locs) if j != k)
+        assert nb == held
+
+
+def test_rccl_one_rank(pkg, oracle):
+    """The RCCL path on a one-GPU box: a real one-rank communicator
+    (gp_comm_unique_id + gp_comm_init), rounds through round_exchange_rccl
+    (the counters' all-reduce), results equal to the oracle's."""
+    g = pkg.overlay.barabasi_albert(5000, 2, seed=9)
+    origin = pkg.overlay.random_origins(g.n, 128, seed=9)
+    inject = (np.arange(128) % 3).astype(np.int32)
+    ref = oracle.run(g, origin, inject, churn=True, p_fail=0.01, churn_seed=2, want_first=True)
+    with pkg.GossipEngine(0, track_first=1, track_msg_forwards=1, churn=1, p_fail=0.01, churn_seed=2) as e:
+        e.load_graph(g)
+        e.comm_init(pkg.GossipEngine.comm_unique_id(), 1, 0)
+        e.set_messages(origin, inject)
+        e.reset()
+        stats = e.run()
+        e.finalize()
+        assert len(stats) == ref["rounds"]
+        for a, b in zip(stats, ref["stats"]):
+            for k in STAT_KEYS:
+                assert a[k] == b[k], (k, a["round"])
+        assert np.array_equal(e.first(), ref["first"])
+        assert np.array_equal(e.digest(), ref["digest"])
+        assert np.array_equal(e.coverage(), ref["coverage"])
+        assert np.array_equal(e.forwards(), ref["forwards"])
+
+
+def test_partitioned_round_needs_an_exchange(pkg):
+    g = pkg.overlay.barabasi_albert(500, 2, seed=1)
+    with pkg.GossipEngine(0) as e:
+        e.load_graph(g)
+        e.set_partition(0, 2)
+        e.set_messages(np.array([3], np.int32))
+        e.reset()
+        with pytest.raises(pkg.GossipError):
+            e.round()
+        with pytest.raises(pkg.GossipError):   # the partition is fixed once per overlay
+            e.set_partition(1, 2)
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
