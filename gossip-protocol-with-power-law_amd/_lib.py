@@ -139,9 +139,8 @@ def load(path=None):
             f"libgossip_hip.so not found at {path}; run __graft_entry__.build() "
             "(the engine has no CPU fallback)")
     try:
-        # RTLD_LOCAL: the PyTorch wheel (imported by the multi-GPU control plane)
-        # bundles its own HIP/RCCL; global symbol interposition between the two
-        # runtimes corrupts the heap at exit, local binding keeps them apart.
+        # RTLD_LOCAL: the C-ABI is reached through ctypes only; nothing else in
+        # the process binds to the library's (or its HIP runtime's) symbols.
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
     except OSError as e:
         raise GossipLibraryError(f"failed to load {path}: {e}") from e

@@ -1,10 +1,13 @@
-"""Multi-process host orchestration on CPU (gloo, world size 2): RCCL-id
-hand-off, partition bounds, ordered gather of owned slices, counter sums.
+"""Multi-process host orchestration on CPU (dist.py's TCP control plane, world
+size 2 and 3): RCCL-id hand-off, partition bounds, ordered gather of owned
+slices, counter sums.
 The per-rank compute is the CPU oracle on the full overlay, sliced as the
 engine slices it; the device exchange itself is covered on the GPU by
 test_gpu_parity.py::test_group_partition_invariance."""
 import os
 import socket
+
+import multiprocessing as mp
 
 import numpy as np
 import pytest
@@ -28,7 +31,7 @@ def _worker(rank, world, port, q):
     from oracle import lib as oracle
     pkg = _gossip_pkg.load()
     d = pkg.dist
-    pg = d.init("gloo")
+    pg = d.init(timeout=120)
     try:
         uid = d.share_comm_id(pg, lambda: bytes(range(128)))
         g = pkg.overlay.barabasi_albert(1001, 2, seed=3)
@@ -43,11 +46,10 @@ def _worker(rank, world, port, q):
         q.put((rank, uid == bytes(range(128)), np.array_equal(first, ref["first"]),
                np.array_equal(digest, ref["digest"]), np.array_equal(cov, ref["coverage"]), tmax))
     finally:
-        pg.destroy_process_group()
+        pg.close()
 
 
 def test_two_rank_gloo_orchestration():
-    mp = pytest.importorskip("torch.multiprocessing")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -82,7 +84,7 @@ def _shard_worker(rank, world, port, q):
     from oracle import lib as oracle
     pkg = _gossip_pkg.load()
     d = pkg.dist
-    pg = d.init("gloo")
+    pg = d.init(timeout=120)
     try:
         g = pkg.overlay.barabasi_albert(700, 2, seed=6)
         m = 200
@@ -108,13 +110,11 @@ def _shard_worker(rank, world, port, q):
         q.put((rank, ok_rounds, np.array_equal(first, full["first"]), np.array_equal(dig, full["digest"]),
                np.array_equal(cov, full["coverage"])))
     finally:
-        pg.destroy_process_group()
+        pg.close()
 
 
 def _gather(pg, x):
-    parts = [None] * pg.get_world_size()
-    pg.all_gather_object(parts, np.asarray(x))
-    return parts
+    return pg.all_gather_array(np.asarray(x))
 
 
 def test_two_rank_message_shards_compose():
@@ -122,7 +122,6 @@ def test_two_rank_message_shards_compose():
     ranks each run the oracle on their word-aligned message block; per-round
     counters sum, first-receipt columns and coverage concatenate and the
     shard digests (global word numbering) XOR to the whole run's."""
-    mp = pytest.importorskip("torch.multiprocessing")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -147,3 +146,58 @@ def test_message_shard_bounds(pkg):
     assert d.message_shard(4096, 8, 3) == (1536, 2048)
     with pytest.raises(ValueError):
         d.message_shard(100, 3, 0)
+
+
+def _plane_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import _gossip_pkg
+    d = _gossip_pkg.load().dist
+    pg = d.init(timeout=120)
+    try:
+        out = []
+        for it in range(50):   # many small collectives back to back keep their order
+            out.append(d.allsum(pg, [rank + it, 1.0])[0])
+        big = d.gather_slices(pg, np.full(100000 + rank, rank, dtype=np.uint64))
+        pg.barrier()
+        mx = d.allmax(pg, 10.0 * rank)
+        q.put((rank, out, big.size, int(big[-1]), mx, "torch" in sys.modules))
+    finally:
+        pg.close()
+
+
+def test_control_plane_three_ranks():
+    """The TCP star with 3 ranks: ordered collectives, a 2.4 MB gather, and no
+    PyTorch in a rank process."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_plane_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out, size, last, mx, torch_loaded in res:
+        assert out == [3 * it + 3 for it in range(50)]
+        assert size == 3 * 100000 + 3 and last == 2 and mx == 20.0
+        assert not torch_loaded
+
+
+def test_bench_imports_no_torch():
+    """The product process (bench.py, the package, the control plane) never
+    imports PyTorch."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import bench, _gossip_pkg; pkg = _gossip_pkg.load(); "
+            "import importlib; importlib.import_module(pkg.__name__ + '.dist'); "
+            "print('torch' in sys.modules)" % root)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "False"
