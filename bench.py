@@ -10,8 +10,8 @@ rounds = 4096 x arcs for a connected overlay) / wall time of the timed steps.
 
 python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 is launched by
 torch.distributed.run (one process per GPU; the data path is RCCL inside
-libgossip_hip.so, torch.distributed/gloo only distributes the RCCL id and the
-timings).
+libgossip_hip.so, the control plane is dist.py's own TCP star, which only
+distributes the RCCL id and the timings: no PyTorch in this process).
 """
 import argparse
 import glob
@@ -57,7 +57,8 @@ def parse():
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--cpu-messages", type=int, default=64)
+    ap.add_argument("--cpu-log2n", type=int, default=20,
+                    help="cpu_baseline: overlay size of the oracle's bounded sample (all messages, W = 64)")
     ap.add_argument("--parallel", choices=("messages", "vertex"), default="messages",
                     help="N > 1: message shards (no data-path collective, default) or the vertex "
                          "partition with an RCCL all-gather of the next rows every round")
@@ -119,24 +120,76 @@ def dense_round_bytes(n, nnz, words):
     return 8 * (n + 1) + 4 * nnz + 8 * words * nnz + 24 * words * n
 
 
+def _host():
+    """Host CPU facts for the cpu_baseline object: the threads this process may
+    use (OMP_NUM_THREADS, else its affinity set), nproc and the CPU model."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or aff
+    return threads, os.cpu_count() or 1, aff, model
+
+
 def cpu_baseline(args, eng, origin, pkg):
-    """The CPU oracle (oracle/gossip_oracle.c, OpenMP) on the same overlay with the
-    first `cpu_messages` of the 4096 messages (one 64-bit word per vertex): a
-    bounded sample of the same workload, in the same unit."""
+    """Two CPU legs, timed on this box's host cores (reported beside the GPU
+    line, never the target):
+      port     oracle/gossip_oracle.c (OpenMP, every thread this process may
+               use) running ALL `messages` (W = 64 words per Message-List row,
+               the GPU's layout) to quiescence on a 2^cpu_log2n-vertex overlay
+               of the same Chung-Lu recipe and seed -- a bounded sample of the
+               workload (the whole 2^24 run would take minutes) in the same unit;
+               this leg is `value`;
+      harness  oracle/harness.py, the reference's per-peer Message-List logic
+               (sha256 digests in a set per peer, Peer.py:175-216, 395-408) plus
+               forwarding, single-core, on BASELINE config 2 (10^4-node BA(m=2),
+               64 messages)."""
+    from oracle import harness
     from oracle import lib as oracle_lib
-    g = eng.graph()
-    threads = args.cpu_threads or min(os.cpu_count() or 1, 16)
-    o = origin[:args.cpu_messages]
-    t0 = time.perf_counter()
+    threads, nproc, aff, model = _host()
+    if args.cpu_threads:
+        threads = args.cpu_threads
     churn = args.workload == "c5"
+    ncpu = 1 << args.cpu_log2n
+    with pkg.GossipEngine(eng.device) as side:   # the same recipe, device-built (bit-identical to the oracle's)
+        side.build_chung_lu(ncpu, args.dbar, args.gamma, args.seed)
+        g = side.graph()
+    o = pkg.overlay.random_origins(ncpu, args.messages, seed=args.seed)
+    t0 = time.perf_counter()
     ref = oracle_lib.run(g, o, nthreads=threads, want_forwards=False, churn=churn,
                          p_fail=args.p_fail if churn else 0.0, churn_seed=args.seed)
     dt = time.perf_counter() - t0
     sends = sum(s["sends"] for s in ref["stats"])
-    return {"value": sends / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
-            "sample": f"oracle/gossip_oracle.c, same 2^{args.log2n}-node overlay, first "
-                      f"{len(o)} of {args.messages} messages, full run{' with churn' if churn else ''} ({ref['rounds']} rounds, "
-                      f"{sends} edge-deliveries, {dt:.1f} s, {threads} OpenMP threads)"}
+    out = {"value": sends / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
+           "sample": f"oracle/gossip_oracle.c, Chung-Lu gamma={args.gamma} d={args.dbar:g} seed {args.seed} at "
+                     f"2^{args.cpu_log2n} vertices ({g.nnz} arcs), all {len(o)} messages (W = 64), full run"
+                     f"{' with churn' if churn else ''} ({ref['rounds']} rounds, {sends} edge-deliveries, "
+                     f"{dt:.1f} s, {threads} OpenMP threads)",
+           "host": {"nproc": nproc, "affinity": aff, "cpu_model": model}}
+    # leg 2: the per-peer Python harness, single core, BASELINE config 2
+    h = pkg.overlay.barabasi_albert(10000, 2, seed=2)
+    ho = pkg.overlay.random_origins(h.n, 64, seed=2).tolist()
+    in_lists = [h.col[h.row_ptr[v]:h.row_ptr[v + 1]].tolist() for v in range(h.n)]
+    t0 = time.perf_counter()
+    hr = harness.run(h.n, in_lists, False, ho, [0] * len(ho))
+    hdt = time.perf_counter() - t0
+    hs = sum(s["sends"] for s in hr["stats"])
+    out["legs"] = [
+        {"kind": "port", "value": out["value"], "unit": "GTEPS", "cores": threads, "sample": out["sample"]},
+        {"kind": "harness", "value": hs / hdt / 1e9, "unit": "GTEPS", "cores": 1,
+         "sample": f"oracle/harness.py (per-peer sha256 Message-List sets), 10^4-node BA(m=2), 64 messages, "
+                   f"{hr['rounds']} rounds, {hs} edge-deliveries, {hdt:.2f} s, 1 core"},
+    ]
+    return out
 
 
 def main():
@@ -145,7 +198,7 @@ def main():
     pkg = _gossip_pkg.load()
     dist = pkg.dist
     world, rank, local = dist.env()
-    pg = dist.init("gloo")
+    pg = dist.init()
     n = 1 << args.log2n
     # one GPU per rank; on a smaller box (rehearsal) ranks share devices round-robin
     device = local % max(pkg._lib.device_count(), 1)
@@ -161,6 +214,10 @@ def main():
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()
+    setup_s = time.perf_counter() - t0
+    # SURVEY.md §8a A9 on the overlay just built (outside the timed region)
+    deg = eng.check_degree(args.gamma)
+    t0 = time.perf_counter()
     shards = world > 1 and args.parallel == "messages"
     if world > 1 and not shards:
         eng.set_partition(rank, world)
@@ -171,12 +228,13 @@ def main():
         eng.set_message_shard(origin, None, lo, hi)
     else:
         eng.set_messages(origin)
-    setup_s = time.perf_counter() - t0
+    setup_s += time.perf_counter() - t0
 
-
-    def step():
+    def step():   # one whole gossip run, including the per-message coverage / forwards pass
         eng.reset()
-        return eng.run()
+        st = eng.run()
+        eng.finalize()
+        return st
 
     for _ in range(args.warmup):
         step()
@@ -240,7 +298,9 @@ def main():
                        "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,
                        "parallelism": (f"message-shard x{world} (no data-path collective)" if shards else
                                        f"vertex-partition x{world}" + (" (RCCL all-gather)" if world > 1 else "")),
-                       "setup_s": round(setup_s, 2)},
+                       "setup_s": round(setup_s, 2),
+                       "degree_check": {"gamma_hat": round(deg["gamma_hat"], 4), "kmin": deg["kmin"],
+                                        "gamma": args.gamma, "ok": bool(deg["ok"])}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": (f"k_expand<{eng.words}>" if eng.words > 32 else
@@ -262,7 +322,7 @@ def main():
         print(json.dumps(out), flush=True)
     eng.close()
     if pg is not None:
-        pg.destroy_process_group()
+        pg.close()
 
 
 if __name__ == "__main__":

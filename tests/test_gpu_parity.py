@@ -172,6 +172,19 @@ def test_chung_lu_device_builder_matches_oracle(pkg, oracle):
         assert np.array_equal(dg.col, col)
 
 
+@pytest.mark.parametrize("n,dbar,seed", [(1_000_000, 8, 3), (1_000_000, 16, 3), (1 << 24, 16, 4)])
+def test_degree_check_on_device_overlays(pkg, n, dbar, seed):
+    """SURVEY.md §8a A9 on the engine's own overlays (C3's recipe, C4's 2^24
+    overlay): the discrete power-law MLE recovers gamma = 2.5 within 0.15
+    (degree-weighted selection is the reference's intent,
+    demonstrate_powerlaw.py:19-27)."""
+    with pkg.GossipEngine(0) as eng:
+        eng.build_chung_lu(n, dbar, 2.5, seed)
+        chk = eng.check_degree(2.5)
+    assert chk["ok"] and abs(chk["gamma_hat"] - 2.5) <= 0.15, chk
+    assert chk["n_tail"] >= 1000 and chk["max_degree"] > 100 * dbar, chk
+
+
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_c3_chung_lu_1e6_1024(pkg, oracle, mode):
     """BASELINE config 3: 10^6-node Chung-Lu (gamma 2.5), 1024 messages."""
