@@ -2432,6 +2432,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
+  bitcount_free(c);
   c->d_msg_fwd = nullptr;
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
   c->inject.clear();
@@ -2690,6 +2691,7 @@ void gp_destroy(gp_ctx* c) {
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_stats);
   dfree(&c->d_hub_items); dfree(&c->d_hubs); dfree(&c->d_hub_item_ptr);
   dfree(&c->d_hub_partial); dfree(&c->d_hub_pnz);
+  bitcount_free(c);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -3215,6 +3217,10 @@ int gp_run(gp_ctx* c, int32_t max_rounds, gp_round_stats* per_round, int32_t* ro
   return 0;
 }
 
+// finalize through the component targets (bitcount.hip); 0: count every row
+#ifndef GP_FINALIZE_BY_COMPONENTS
+#define GP_FINALIZE_BY_COMPONENTS 1
+#endif
 int gp_finalize_messages(gp_ctx* c) {
   if (!c) return set_error(GP_EINVAL, "null ctx");
   if (!state_ready(c)) return set_error(GP_ESTATE, "no run state");
@@ -3226,17 +3232,10 @@ int gp_finalize_messages(gp_ctx* c) {
   u64* gcov = c->d_msg_cov + 2 * M;
   u64* gfwd = c->d_msg_cov + 3 * M;
   const bool fwd_from_seen = !c->liveness_active && !c->cfg.track_msg_forwards;
-  GP_HIP(hipMemsetAsync(cov, 0, M * 8, s));
-  if (fwd_from_seen) GP_HIP(hipMemsetAsync(fwd_local, 0, M * 8, s));
-  BitsumArgs b{};
-  b.slot[0] = c->d_slot[0];   // seen row i = slot[sp[i]][i], owned local ids [0, nloc)
-  b.slot[1] = c->d_slot[1];
-  b.sel = c->d_sp;
-  b.weight = c->d_deg_out;
-  b.cnt = cov;
-  b.wsum = fwd_from_seen ? fwd_local : nullptr;
-  b.count = c->nloc();
-  GP_TRY(launch_bitsum(c, b, true, fwd_from_seen));
+  // seen row i = slot[sp[i]][i], owned local ids [0, nloc): bit-sliced counts
+  // (bitcount.hip), forwards weighted by the static degree (= deg_live without liveness)
+  if (c->done_at_valid && GP_FINALIZE_BY_COMPONENTS) GP_TRY(finalize_by_components(c, fwd_from_seen, cov, fwd_local));
+  else GP_TRY(bitcount_messages(c, fwd_from_seen, cov, fwd_local));
   if (c->comm) {
     GP_RCCL(ncclGroupStart());
     GP_RCCL(ncclAllReduce(cov, gcov, M, ncclUint64, ncclSum, c->comm, s));

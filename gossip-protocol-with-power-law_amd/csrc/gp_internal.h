@@ -175,6 +175,13 @@ struct Ctx {
   u64* d_msg_cov = nullptr;    // [W*64]
   u64* d_msg_fwd = nullptr;    // [W*64]
   u64* d_alive = nullptr;      // [2][W] alive messages per round parity
+  u64* d_bc_keys = nullptr;    // [nloc] (degree << 32 | v) sorted: weighted bitcount order (bitcount.hip)
+  uint32_t* d_bc_part = nullptr;   // per-block bitcount partials
+  size_t bc_part_words = 0;
+  int64_t bc_split = 0;        // owned vertices of degree <= the bitcount tail threshold
+  u64* d_fin_comp = nullptr;   // finalize by components: [K] counts, [K] degree sums, list cursor
+  u64* d_fin_list = nullptr;   // [nloc] incomplete rows (degree << 32 | v)
+  int32_t fin_comp_rows = 0;
   gp_report* d_reports = nullptr;
   int64_t report_cap = 0;
   u64* d_stats = nullptr;      // [NSTAT]
@@ -251,6 +258,10 @@ int build_gather_order(Ctx* c);
 // gossip_engine.hip
 int finish_graph(Ctx* c);
 int build_hubs(Ctx* c);
+// bitcount.hip
+int bitcount_messages(Ctx* c, bool weighted, u64* cov, u64* fwd);   // coverage / forwards of the owned rows
+int finalize_by_components(Ctx* c, bool weighted, u64* cov, u64* fwd);   // the same via cmask rows
+void bitcount_free(Ctx* c);
 // partition.hip
 int localize(Ctx* c);                          // global overlay -> owned + ghost local CSR, boundary lists
 int set_extras(Ctx* c, const std::vector<int32_t>& origins_global);   // origins neither owned nor ghosts

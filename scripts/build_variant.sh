@@ -10,7 +10,9 @@ F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 $2"
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/gossip_engine.hip -o $OUT/ge.o &
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/graph_build.hip -o $OUT/gb.o &
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/checkpoint.hip -o $OUT/ck.o &
+/opt/rocm/bin/hipcc $F -c $PKG/csrc/partition.hip -o $OUT/pt.o &
+/opt/rocm/bin/hipcc $F -c $PKG/csrc/bitcount.hip -o $OUT/bc.o &
 wait
-/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o $OUT/ck.o -o $PKG/_variants/$1.so -lrccl
+/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o $OUT/ck.o $OUT/pt.o $OUT/bc.o -o $PKG/_variants/$1.so -lrccl
 rm -rf $OUT
 echo $PKG/_variants/$1.so

@@ -1,0 +1,62 @@
+"""The multi-process launch of bench.py on the GPU box: real engine processes
+(one context each, both on cuda:0 of the one-GPU box) over dist.py's TCP
+control plane, message shards.  The 2-rank whole-job
+edge-deliveries must equal the 1-rank run's, and neither process may load
+PyTorch."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--log2n", "16", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(world, extra=()):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GP_CTRL_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(world),
+                                       *ARGS, *extra], env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=180)
+        assert p.returncode == 0, e[-3000:]
+        outs.append(o)
+    lines = [json.loads(x) for x in outs[0].splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and all(not o.strip() for o in outs[1:])
+    return lines[0]
+
+
+def test_two_process_message_shards():
+    one = _launch(1)
+    two = _launch(2)
+    assert two["n_gpus"] == 2 and "message-shard x2" in two["config"]["parallelism"]
+    for k in ("n", "arcs", "messages", "edge_deliveries_per_step", "rounds_per_step"):
+        assert two["config"][k] == one["config"][k], k
+    assert two["config"]["words_per_row"] == 32 and one["config"]["words_per_row"] == 64
+
+
+def test_bench_process_loads_no_torch():
+    code = ("import runpy, sys; sys.argv = ['bench.py'] + %r; "
+            "runpy.run_path('bench.py', run_name='__main__'); "
+            "sys.stderr.write('TORCH=%%s\\n' %% ('torch' in sys.modules))" % (ARGS,))
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "TORCH=False" in p.stderr
