@@ -380,7 +380,9 @@ int bitcount_messages(Ctx* c, bool weighted, u64* cov, u64* fwd) {
 // grid-stride over 64-vertex chunks per wave; a wave keeps the running count
 // and degree sum of one component (the giant one, in practice) in registers
 // and adds them once at the end -- per-chunk atomics on that one address were
-// 0.5 M same-address adds at C4 (3.2 ms); other components add per chunk
+// 0.5 M same-address adds at C4 (3.2 ms); other components add per chunk.
+// First pass (list null): component sums + the number of incomplete rows;
+// second pass (only when few): list them.
 __global__ __launch_bounds__(BC_BLOCK) void k_fin_scan(const uint32_t* __restrict__ seenpop,
                                                        const uint32_t* __restrict__ done_at,
                                                        const int32_t* __restrict__ midx,
@@ -391,6 +393,7 @@ __global__ __launch_bounds__(BC_BLOCK) void k_fin_scan(const uint32_t* __restric
   const int64_t nwaves = (int64_t)gridDim.x * BC_WAVES;
   int32_t kr = -1;       // the wave's running component
   u64 rc = 0, rd = 0;    // its count and degree sum (wave-uniform)
+  u64 npart = 0;         // incomplete rows seen by the wave
   for (int64_t base = ((int64_t)blockIdx.x * BC_WAVES + (threadIdx.x >> 6)) * 64; base < n; base += nwaves * 64) {
     const int64_t v = base + lane;
     bool full = false, part = false;
@@ -415,7 +418,8 @@ __global__ __launch_bounds__(BC_BLOCK) void k_fin_scan(const uint32_t* __restric
       u64 ds = mine ? d : 0ull;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) ds += __shfl_xor(ds, o);
-      if (kl == kr) {
+      if (list) {   // second pass: the component sums are in already
+      } else if (kl == kr) {
         rc += (u64)__popcll(mm);
         rd += ds;
       } else if (lane == leader) {
@@ -425,17 +429,28 @@ __global__ __launch_bounds__(BC_BLOCK) void k_fin_scan(const uint32_t* __restric
       fm &= ~mm;
     }
     const u64 pm = __ballot(part);
-    if (pm) {
+    if (list && pm) {   // second pass: few incomplete rows, list them
       const int first = __ffsll((long long)pm) - 1;
       u64 at = 0;
       if (lane == first) at = atomicAdd(list_n, (u64)__popcll(pm));
       at = __shfl(at, first);
       if (part) list[at + (u64)__popcll(pm & ((1ull << lane) - 1ull))] = (d << 32) | (u64)(uint32_t)v;
     }
+    npart += (u64)__popcll(pm);
   }
-  if (kr >= 0 && lane == 0) {
-    atomicAdd(&comp_cnt[kr], rc);
-    atomicAdd(&comp_deg[kr], rd);
+  if (!list) {   // first pass: count the incomplete rows, one atomic per block
+    __shared__ u64 bsum[BC_WAVES];
+    if (lane == 0) bsum[threadIdx.x >> 6] = npart;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      u64 t = 0;
+      for (int k = 0; k < BC_WAVES; ++k) t += bsum[k];
+      if (t) atomicAdd(list_n, t);
+    }
+    if (kr >= 0 && lane == 0) {
+      atomicAdd(&comp_cnt[kr], rc);
+      atomicAdd(&comp_deg[kr], rd);
+    }
   }
 }
 
@@ -468,20 +483,28 @@ int finalize_by_components(Ctx* c, bool weighted, u64* cov, u64* fwd) {
     GP_TRY(dalloc(&c->d_fin_comp, 2 * (size_t)K + 1));
     c->fin_comp_rows = K;
   }
-  if (!c->d_fin_list) GP_TRY(dalloc(&c->d_fin_list, (size_t)std::max<int64_t>(n, 1)));
   u64* comp_cnt = c->d_fin_comp;
   u64* comp_deg = c->d_fin_comp + K;
   u64* list_n = c->d_fin_comp + 2 * (size_t)K;
   GP_HIP(hipMemsetAsync(c->d_fin_comp, 0, (2 * (size_t)K + 1) * 8, s));
+  const dim3 sg((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + BC_BLOCK - 1) / BC_BLOCK,
+                                                                   (int64_t)c->cu_count * 8)));
   if (n > 0)
-    hipLaunchKernelGGL(k_fin_scan,
-                       dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + BC_BLOCK - 1) / BC_BLOCK,
-                                                                             (int64_t)c->cu_count * 8))),
-                       dim3(BC_BLOCK), 0, s,
-                       c->d_seenpop, c->d_done_at, c->d_midx, c->d_deg_out, n, comp_cnt, comp_deg, c->d_fin_list,
-                       list_n);
+    hipLaunchKernelGGL(k_fin_scan, sg, dim3(BC_BLOCK), 0, s, c->d_seenpop, c->d_done_at, c->d_midx, c->d_deg_out, n,
+                       comp_cnt, comp_deg, (u64*)nullptr, list_n);
+  u64 incomplete = 0;
+  GP_TRY(copy_sync(c, &incomplete, list_n, 8, hipMemcpyDeviceToHost));
+  // many incomplete rows (churn: crashes cut messages off, so nobody completes
+  // its component): the bit-sliced pass over every row is the cheaper way
+  if ((int64_t)incomplete * 32 > n) return bitcount_messages(c, weighted, cov, fwd);
   hipLaunchKernelGGL(k_fin_comp, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, c->d_cmask, c->cmask_rows, W,
                      comp_cnt, comp_deg, cov, weighted ? fwd : nullptr);
+  GP_HIP(hipGetLastError());
+  if (incomplete == 0) return 0;
+  if (!c->d_fin_list) GP_TRY(dalloc(&c->d_fin_list, (size_t)std::max<int64_t>(n, 1)));
+  GP_HIP(hipMemsetAsync(list_n, 0, 8, s));
+  hipLaunchKernelGGL(k_fin_scan, sg, dim3(BC_BLOCK), 0, s, c->d_seenpop, c->d_done_at, c->d_midx, c->d_deg_out, n,
+                     comp_cnt, comp_deg, c->d_fin_list, list_n);
   BitcountArgs a{};
   a.slot[0] = c->d_slot[0];
   a.slot[1] = c->d_slot[1];

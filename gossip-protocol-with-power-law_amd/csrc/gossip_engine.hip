@@ -17,6 +17,8 @@
 //   seenpop        u32[nloc]         |seen(v)| -> vertices holding all m skip E_r
 //   in-CSR         i64 row_ptr[n+1], i32 col[nnz]
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -3217,10 +3219,12 @@ int gp_run(gp_ctx* c, int32_t max_rounds, gp_round_stats* per_round, int32_t* ro
   return 0;
 }
 
-// finalize through the component targets (bitcount.hip); 0: count every row
-#ifndef GP_FINALIZE_BY_COMPONENTS
-#define GP_FINALIZE_BY_COMPONENTS 1
-#endif
+// finalize through the component targets (bitcount.hip); GP_FINALIZE_ROWS=1 in
+// the environment counts every row instead (the tests compare the two)
+static bool finalize_by_rows() {
+  const char* e = getenv("GP_FINALIZE_ROWS");
+  return e && e[0] == '1';
+}
 int gp_finalize_messages(gp_ctx* c) {
   if (!c) return set_error(GP_EINVAL, "null ctx");
   if (!state_ready(c)) return set_error(GP_ESTATE, "no run state");
@@ -3234,7 +3238,7 @@ int gp_finalize_messages(gp_ctx* c) {
   const bool fwd_from_seen = !c->liveness_active && !c->cfg.track_msg_forwards;
   // seen row i = slot[sp[i]][i], owned local ids [0, nloc): bit-sliced counts
   // (bitcount.hip), forwards weighted by the static degree (= deg_live without liveness)
-  if (c->done_at_valid && GP_FINALIZE_BY_COMPONENTS) GP_TRY(finalize_by_components(c, fwd_from_seen, cov, fwd_local));
+  if (c->done_at_valid && !finalize_by_rows()) GP_TRY(finalize_by_components(c, fwd_from_seen, cov, fwd_local));
   else GP_TRY(bitcount_messages(c, fwd_from_seen, cov, fwd_local));
   if (c->comm) {
     GP_RCCL(ncclGroupStart());

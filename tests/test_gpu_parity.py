@@ -697,3 +697,45 @@ def test_checkpoint_rejected_blob_leaves_run_intact(pkg, oracle, tmp_path):
     assert np.array_equal(a.digest(), ref["digest"])
     assert np.array_equal(a.forwards(), ref["forwards"])
     a.close()
+
+
+@pytest.mark.parametrize("m,churn", [(64, None), (1000, None), (4096, None), (300, "random"), (4096, "random"),
+                                     (200, "few"), (4096, "few")])
+def test_finalize_paths_agree(pkg, oracle, m, churn, monkeypatch):
+    """gp_finalize_messages through the component targets (complete vertices
+    add their component's mask row; a few incomplete rows -- explicit crashes --
+    bit by bit from a list; many -- random churn -- the bit-sliced pass over
+    every row) against the bit-sliced pass forced (GP_FINALIZE_ROWS=1) and the
+    oracle, at widths 1..64."""
+    g = pkg.overlay.barabasi_albert(3000, 2, seed=11)
+    origin = pkg.overlay.random_origins(g.n, m, seed=11)
+    cfg = dict(track_digest=1)
+    okw = {}
+    crashes = []
+    if churn == "random":
+        cfg.update(churn=1, p_fail=0.02, churn_seed=7, track_msg_forwards=1)
+        okw = dict(churn=True, p_fail=0.02, churn_seed=7)
+    elif churn == "few":
+        cfg.update(track_msg_forwards=1)
+        crashes = [(int(v), 2) for v in range(100, 3000, 300)]
+        okw = dict(crashes=crashes)
+    with pkg.GossipEngine(0, **cfg) as eng:
+        eng.load_graph(g)
+        eng.set_messages(origin)
+        eng.reset()
+        for r in range(254):
+            if crashes and r == 2:
+                eng.crash([v for v, _ in crashes])
+            st = eng.round()
+            if st["new_bits"] == 0 and r >= 0:
+                break
+        monkeypatch.delenv("GP_FINALIZE_ROWS", raising=False)
+        eng.finalize()
+        cov_c, fwd_c = eng.coverage(), eng.forwards()
+        monkeypatch.setenv("GP_FINALIZE_ROWS", "1")
+        eng.finalize()
+        cov_r, fwd_r = eng.coverage(), eng.forwards()
+        monkeypatch.delenv("GP_FINALIZE_ROWS")
+    ref = oracle.run(g, origin, **okw)
+    assert np.array_equal(cov_c, ref["coverage"]) and np.array_equal(cov_r, ref["coverage"])
+    assert np.array_equal(fwd_c, ref["forwards"]) and np.array_equal(fwd_r, ref["forwards"])
