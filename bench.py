@@ -214,7 +214,7 @@ def main():
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()
-    setup_s = time.perf_counter() - t0
+    setup_s = build_s = time.perf_counter() - t0
     # SURVEY.md §8a A9 on the overlay just built (outside the timed region)
     deg = eng.check_degree(args.gamma)
     t0 = time.perf_counter()
@@ -298,7 +298,7 @@ def main():
                        "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,
                        "parallelism": (f"message-shard x{world} (no data-path collective)" if shards else
                                        f"vertex-partition x{world}" + (" (RCCL all-gather)" if world > 1 else "")),
-                       "setup_s": round(setup_s, 2),
+                       "setup_s": round(setup_s, 2), "build_s": round(build_s, 2),
                        "degree_check": {"gamma_hat": round(deg["gamma_hat"], 4), "kmin": deg["kmin"],
                                         "gamma": args.gamma, "ok": bool(deg["ok"])}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1,10 +1,10 @@
 #!/bin/bash
 # build an experimental libgossip_hip.so variant: build_variant.sh NAME "-DFLAG=..."
-# output: gossip-protocol-with-power-law_amd/_variants/NAME.so (git-ignored)
+# output: gossip-protocol-with-power-law_amd/_ab/NAME.so (git-ignored, travels to the GPU box)
 set -e
 cd "$(dirname "$0")/.."
 PKG=gossip-protocol-with-power-law_amd
-OUT=$PKG/_variants/$1
+OUT=$PKG/_ab/$1
 mkdir -p $OUT
 F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 $2"
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/gossip_engine.hip -o $OUT/ge.o &
@@ -13,6 +13,6 @@ F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 $2"
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/partition.hip -o $OUT/pt.o &
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/bitcount.hip -o $OUT/bc.o &
 wait
-/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o $OUT/ck.o $OUT/pt.o $OUT/bc.o -o $PKG/_variants/$1.so -lrccl
+/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o $OUT/ck.o $OUT/pt.o $OUT/bc.o -o $PKG/_ab/$1.so -lrccl
 rm -rf $OUT
-echo $PKG/_variants/$1.so
+echo $PKG/_ab/$1.so
