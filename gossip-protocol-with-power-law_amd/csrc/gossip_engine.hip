@@ -738,6 +738,92 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   st.add(S_WRITTEN, 1);
 }
 
+// SCAN_PRE rounds without early exit (round 1 of a C4 run: 7.9 M receivers,
+// about 2 active in-neighbours each, already found by the lane phase): two
+// receivers per wave, one per half.  A half-wave loads a whole 64-word row per
+// instruction, so each receiver keeps its rows in flight on its own and the
+// chain rows -> commit is walked for two receivers at a time.  Same commits
+// as finish_row (deferred per-vertex words in L.tot / L.dig).
+#ifndef GP_PRE_PAIRS
+#define GP_PRE_PAIRS 1
+#endif
+template <int W, class LDS>
+__device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
+                                          WaveStats& st) {
+  static_assert(W == 64, "half-wave rows");
+  const int lane = threadIdx.x & 63, h = lane >> 5, lw = lane & 31;
+  while (mp) {
+    const int kA = __ffsll((long long)mp) - 1;
+    mp &= mp - 1;
+    int kB = -1;
+    if (mp) {
+      kB = __ffsll((long long)mp) - 1;
+      mp &= mp - 1;
+    }
+    const bool on = h == 0 || kB >= 0;
+    const int ks = (h && kB >= 0) ? kB : kA;
+    const uint32_t npA = L.np[kA], npB = kB >= 0 ? (uint32_t)L.np[kB] : 0u;
+    const uint32_t np = on ? (h ? npB : npA) : 0u;
+    const int64_t i = base + ks;
+    const int v = (int)(a.vbegin + i);
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
+    u64x2 acc = {0, 0};
+    const uint32_t nmax = max(npA, npB);
+    for (uint32_t q0 = 0; q0 < nmax; q0 += GP_ROWS_IN_FLIGHT) {
+      u64x2 r[GP_ROWS_IN_FLIGHT];
+#pragma unroll
+      for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
+        r[q] = u64x2{0, 0};
+        if (q0 + q < np) r[q] = load_piece<W>(a.rows, L.pre[ks][q0 + q], lw);
+      }
+#pragma unroll
+      for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
+    }
+    st.add(S_GATHERED, (u64)(npA + npB));
+    st.add(S_ROW_BYTES, (u64)(npA + npB) * (u64)(8 * W));
+    const u64 bz = __ballot(on && (acc.x | acc.y) != 0ull);
+    const bool any_h = ((bz >> (32 * h)) & 0xFFFFFFFFull) != 0ull;
+    u64x2 sv = {0, 0};
+    if (any_h && sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
+    {
+      const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
+      const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
+      st.add(S_SEEN_READ, (u64)(((bz & 0xFFFFFFFFull) && sA != SLOT_NONE) ? 1 : 0) +
+                              (u64)(((bz >> 32) && kB >= 0 && sB != SLOT_NONE) ? 1 : 0));
+    }
+    const u64x2 nw = acc & ~sv;
+    uint32_t tot = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
+    u64 t = 0;
+    if (on && tot) {
+      alive_add<W>(a, L, lw, nw);
+      store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);
+      if (a.frx_next) store_piece<W>(a.frx_next, v, lw, nw);
+      if (a.first) {
+        uint8_t* row = a.first + (size_t)i * (W * 64);
+        if (nw.x) set_first_bytes(row, 2 * lw, nw.x, (uint32_t)a.rr);
+        if (nw.y) set_first_bytes(row, 2 * lw + 1, nw.y, (uint32_t)a.rr);
+      }
+      if (a.digest) {
+        if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 2 * lw), nw.x);
+        if (nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 2 * lw + 1), nw.y);
+      }
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) t ^= __shfl_xor(t, o);
+    if (lw == 0 && on && tot) {
+      L.tot[ks] = tot;
+      L.dig[ks] = t;
+    }
+    const uint32_t tA = (uint32_t)__builtin_amdgcn_readlane((int)tot, 0);
+    const uint32_t tB = kB >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)tot, 32) : 0u;
+    st.add(S_NEW_BITS, (u64)tA + (u64)tB);
+    st.add(S_RECEIVERS, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
+    st.add(S_WRITTEN, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
+  }
+}
+
 // k_expand's commit of the deferred per-vertex words: lane k holds vertex
 // base + k (need: it was scanned)
 template <class LDS>
@@ -861,6 +947,13 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     wave_sync_lds();
     const bool ee = a.early_exit != 0;
     u64 m = __ballot(need);
+    if constexpr (GP_PRE_PAIRS && W == 64 && (MODE & 3) == SCAN_PRE && (MODE & SCAN_CML) == 0) {
+      if (!ee) {   // prefiltered receivers two at a time, the rest below
+        const u64 mp = __ballot(need && L.np[lane] != 0xFFu);
+        pre_pairs<W>(a, L, mp, base, slot_of, st);
+        m &= ~mp;
+      }
+    }
     while (m) {
       const int k = __ffsll((long long)m) - 1;
       m &= m - 1;
