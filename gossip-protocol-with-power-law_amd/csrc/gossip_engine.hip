@@ -183,10 +183,10 @@ struct ExpandArgs {
   const u64* __restrict__ alive;       // [W] messages some sender forwards this round (or null)
   u64* __restrict__ alive_next;        // [W] the same for round r + 1: OR of the new rows (or null)
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
-  const u64* __restrict__ cmk;         // compact-list masks of this round's senders (or null):
-                                       //   0 = not a sender, CML_DENSE = full row, else the mask
-  const u64* __restrict__ cml;         // their compact records
-  u64* __restrict__ cmk_next;          // masks / records the receivers write (or null)
+  const u64* __restrict__ cmk;         // record rounds: dense bitmap of this round's senders (bit v:
+                                       //   read v's full row) (or null)
+  const u64* __restrict__ cml;         // their records (word 0 mask, then the nonzero words)
+  u64* __restrict__ cmk_next;          // dense bitmap / records the receivers write (or null)
   u64* __restrict__ cml_next;
   const uint32_t* __restrict__ done_at;// |messages of v's component|: seenpop == done_at -> done
   uint32_t* __restrict__ fpop_next;
@@ -224,14 +224,16 @@ struct ExpandArgs {
 
 constexpr uint8_t SLOT_NONE = 0xFF;
 
-// compact Message-Lists (W = 64): per vertex a mask word
-// (cmk: bit w = word w of its Message-List is nonzero; 0 = not a sender this
-// round; CML_DENSE = more than CML_WORDS nonzero words, read the full row) and
-// a 128-B record holding the nonzero words in order.  Sparse rounds probe the
-// mask instead of the activity bitmap and gather one line per sender instead
-// of four.
-constexpr int CML_WORDS = 16;
-constexpr u64 CML_DENSE = ~0ull;
+// Message-List records (W = 64): a round whose receivers end
+// up with sparse Message-Lists also writes, per receiver, a 128-B record --
+// word 0 the mask of its nonzero words (bit w = word w), then those words in
+// order (at most CML_MAXW) -- or sets its bit in a dense bitmap (more nonzero
+// words: read the full row).  The next round, a filtered pull, probes the
+// dense bitmap beside the activity bitmap (both 2 MB at 2^24, L2-resident) and
+// gathers one 128-B line per sparse sender instead of four, four senders per
+// wave-instruction.
+constexpr int CML_WORDS = 16;             // u64 per record
+constexpr int CML_MAXW = CML_WORDS - 1;   // nonzero words a record holds
 
 // occupancy target of k_expand (waves per SIMD; 0 = compiler's choice)
 #ifndef GP_DETECT_BLOCKS_PER_CU
@@ -269,8 +271,9 @@ struct WaveLdsT {
   u64 dig[64];          // k_expand: digest terms of vertex k
   int64_t rp[65];       // k_expand: row_ptr of the wave's vertices (rp[k], rp[k + 1])
   int32_t mi[64];       // k_expand: component-mask row of vertex k (early-exit rounds)
-  u64 msk[CML ? 64 : 1];          // compact-row rounds: the staged senders' record masks
-  u64 cm[CML ? 64 : 1];           // compact-row rounds: mask word of the wave's vertex k (committed)
+  u64 racc[CML ? 64 : 1];         // record rounds: OR of the gathered records, word w
+  int32_t sid[CML ? 64 : 1];      // record rounds: sparse senders of one pass
+  uint8_t cd[CML ? 64 : 1];       // record-writing rounds: vertex k's row is dense (no record)
   int32_t pre[PRE ? 64 : 1][PRE_IDS];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
   uint8_t np[PRE ? 64 : 1];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
   u64 alive[64];                  // OR of the new rows this wave wrote (alive_next)
@@ -468,55 +471,43 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* 
   return gather_rows_n<W, GP_ROWS_IN_FLIGHT>(a, idx, cnt, g, lw, acc, st, ee, want);
 }
 
-// compact-row rounds: the staged senders' record masks into L.msk (one
-// instruction for the pass), and the record/row bytes they stand for
-template <int W, class LDS>
-__device__ __forceinline__ void stage_masks(const ExpandArgs& a, LDS& L, const int32_t* idx, int cnt,
-                                            WaveStats& st) {
-  const int lane = threadIdx.x & 63;
-  u64 bytes = 0;
-  if (lane < cnt) {
-    const u64 m = a.cmk[idx[lane]];
-    L.msk[lane] = m;
-    bytes = m == CML_DENSE ? (u64)(8 + 8 * W) : (u64)(8 + 8 * __popcll(m));
+// position of the k-th (1-based) set bit of m
+__device__ __forceinline__ int select_bit(u64 m, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int sh = 32; sh > 0; sh >>= 1) {
+    const int c = __popcll(m & ((1ull << sh) - 1ull));
+    if (c < k) {
+      k -= c;
+      m >>= sh;
+      pos += sh;
+    }
   }
-  st.add(S_ROW_BYTES, wave_sum_u64(bytes));
-  wave_sync_lds();
+  return pos;
 }
 
-// gather_rows over compact records (no early exit: sparse rounds only).  Lane
-// (g, lw) holds words 2lw, 2lw + 1: from a compact record it loads the packed
-// entries of those words if they are nonzero, from a dense sender its piece.
-template <int W, class LDS>
-__device__ __forceinline__ void gather_rows_cml(const ExpandArgs& a, const LDS& L, const int32_t* idx, int cnt,
-                                                int g, int lw, u64x2& acc, WaveStats& st) {
-  constexpr int RPI = Geo<W>::RPI;
-  static_assert(W == 64, "compact records hold 64-word rows");
-  const int w0 = 2 * lw;
-  const u64 below = (1ull << w0) - 1ull;   // words below w0
-  for (int k0 = 0; k0 < cnt; k0 += GP_ROWS_IN_FLIGHT * RPI) {
-    u64x2 r[GP_ROWS_IN_FLIGHT];
+// records of the staged sparse senders idx[0, cnt): a 16-lane group loads one
+// 128-B record (lane 0 of the group its mask), GP_ROWS_IN_FLIGHT records per
+// group in flight; each word is OR-ed into L.racc at its word index.
+template <class LDS>
+__device__ __forceinline__ void gather_recs(const ExpandArgs& a, LDS& L, const int32_t* idx, int cnt,
+                                            WaveStats& st) {
+  const int lane = threadIdx.x & 63, gq = lane >> 4, sl = lane & 15;
+  for (int k0 = 0; k0 < cnt; k0 += 4 * GP_ROWS_IN_FLIGHT) {
+    u64 val[GP_ROWS_IN_FLIGHT];
 #pragma unroll
     for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
-      const int k = k0 + g + q * RPI;
-      r[q] = u64x2{0, 0};
-      if (k < cnt) {
-        const int32_t u = idx[k];
-        const u64 m = L.msk[k];
-        if (m == CML_DENSE) {
-          r[q] = load_piece<W>(a.rows, u, lw);
-        } else {
-          const u64* rec = a.cml + (size_t)u * CML_WORDS;
-          const int p = __popcll(m & below);
-          if ((m >> w0) & 1ull) r[q].x = rec[p];
-          if ((m >> (w0 + 1)) & 1ull) r[q].y = rec[p + (int)((m >> w0) & 1ull)];
-        }
-      }
+      const int k = k0 + 4 * q + gq;
+      val[q] = k < cnt ? a.cml[(size_t)idx[k] * CML_WORDS + sl] : 0ull;
     }
 #pragma unroll
-    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
-    st.add(S_GATHERED, (u64)min(GP_ROWS_IN_FLIGHT * RPI, cnt - k0));
+    for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
+      const u64 m = __shfl(val[q], lane & ~15);
+      if (sl >= 1 && sl <= __popcll(m) && val[q]) atomicOr(&L.racc[select_bit(m, sl)], val[q]);
+    }
   }
+  st.add(S_GATHERED, (u64)cnt);
+  st.add(S_ROW_BYTES, (u64)cnt * (u64)(8 * CML_WORDS));
 }
 
 // stage one pass of probed neighbours (e: this lane's entry, -1 = none) in
@@ -563,26 +554,22 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
     st.add(S_ARCS, n);
     int cnt;
     if constexpr (W == 64 && (MODE & SCAN_CML) != 0) {
-      if (a.cmk) {   // sparse round: the mask array is the probe (no early exit here)
+      if (a.cmk) {   // record round (no early exit): sparse senders' records, dense senders' rows
         int32_t u = -1;
-        u64 m = 0;
+        bool act = false, dense = false;
         if (lane < n) {
           u = a.gcol[j0 + lane];
-          m = a.cmk[u];
+          act = probe<MODE>(a, u) >= 0;
+          if (act) dense = ((a.cmk[u >> 6] >> (u & 63)) & 1ull) != 0ull;
         }
-        const u64 am = __ballot(m != 0ull);
-        u64 bytes = 0;
-        if (m) {
-          const int r = lane_rank(am);
-          L.idx[r] = u;
-          L.msk[r] = m;
-          bytes = m == CML_DENSE ? (u64)(8 * W) : (u64)(8 * __popcll(m));
+        const u64 md = __ballot(act && dense), ms = __ballot(act && !dense);
+        if (act) {
+          if (dense) L.idx[lane_rank(md)] = u;
+          else L.sid[lane_rank(ms)] = u;
         }
-        st.add(S_ROW_BYTES, wave_sum_u64(bytes));
         wave_sync_lds();
-        cnt = __popcll(am);
-        if (cnt == 0) continue;
-        gather_rows_cml<W>(a, L, L.idx, cnt, g, lw, acc, st);
+        if (md) gather_rows<W>(a, L.idx, __popcll(md), g, lw, acc, st, false, want);
+        if (ms) gather_recs(a, L, L.sid, __popcll(ms), st);
         wave_sync_lds();
         continue;
       }
@@ -635,20 +622,26 @@ __device__ __forceinline__ u64 spread32(u64 x) {
   x = (x | (x << 1)) & 0x5555555555555555ull;
   return x;
 }
-// the compact record of a 64-word Message-List held as (g, lw) pieces by the
-// group-0 lanes (W = 64: lanes 0..31, words 2lw and 2lw + 1)
-// returns the vertex's mask word (uniform)
-__device__ __forceinline__ u64 write_cml(u64* __restrict__ cml, int v, int g, int lw, u64x2 row) {
+// the record of a 64-word Message-List held as (g, lw) pieces by the group-0
+// lanes (W = 64: lanes 0..31, words 2lw and 2lw + 1); returns true (uniform)
+// when the row is dense and no record is written
+__device__ __forceinline__ bool write_rec(u64* __restrict__ cml, int v, int g, int lw, u64x2 row) {
   const u64 bx = __ballot(g == 0 && row.x != 0ull), by = __ballot(g == 0 && row.y != 0ull);
   const u64 m = spread32(bx) | (spread32(by) << 1);
-  if (__popcll(m) > CML_WORDS) return CML_DENSE;
+  if (__popcll(m) > CML_MAXW) return true;
   u64* rec = cml + (size_t)v * CML_WORDS;
   if (g == 0) {
-    const int p = __popcll(m & ((1ull << (2 * lw)) - 1ull));
+    const int p = 1 + __popcll(m & ((1ull << (2 * lw)) - 1ull));
     if (row.x) rec[p] = row.x;
     if (row.y) rec[p + (row.x ? 1 : 0)] = row.y;
+    if (lw == 0) rec[0] = m;
   }
-  return m;
+  return false;
+}
+
+// dense bit of vertex v in a record-writing round (one atomic: hubs, push)
+__device__ __forceinline__ void set_dense(u64* __restrict__ bm, int v) {
+  atomicOr(bm + (v >> 6), 1ull << (v & 63));
 }
 
 // receiver side of vertex v (local index i): new = acc & ~seen; write the new
@@ -665,10 +658,7 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
-    if (!DEFER && lane == 0) {
-      a.fpop_next[v] = 0;
-      if (CMLW && a.cmk_next) a.cmk_next[v] = 0;
-    }
+    if (!DEFER && lane == 0) a.fpop_next[v] = 0;
     return;
   }
   if (!have_sv && sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
@@ -685,15 +675,12 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   const uint32_t pc = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
   const uint32_t tot = wave_sum_u32(pc);
   if (tot == 0) {
-    if (!DEFER && lane == 0) {
-      a.fpop_next[v] = 0;
-      if (CMLW && a.cmk_next) a.cmk_next[v] = 0;
-    }
+    if (!DEFER && lane == 0) a.fpop_next[v] = 0;
     return;
   }
-  u64 cm = 0;
+  bool dense = true;
   if constexpr (W == 64 && CMLW) {
-    if (a.cml_next) cm = write_cml(a.cml_next, v, g, lw, sv | nw);
+    if (a.cml_next) dense = write_rec(a.cml_next, v, g, lw, sv | nw);
   }
   if (g == 0) {
     alive_add<W>(a, L, lw, nw);
@@ -721,11 +708,11 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   if constexpr (DEFER) {
     if (lane == 0) {
       L.tot[k] = tot;
-      if constexpr (CMLW && LDS::kCml) L.cm[k] = cm;
+      if constexpr (CMLW && LDS::kCml) L.cd[k] = dense ? 1 : 0;
     }
   } else {
     if (lane == 0) {
-      if (CMLW && a.cmk_next) a.cmk_next[v] = cm;
+      if (a.cmk_next) set_dense(a.cmk_next, v);
       a.fpop_next[v] = tot;
       a.seenpop[i] += tot;
       a.sp[v] = (uint8_t)a.wslot;
@@ -796,6 +783,22 @@ __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
     u64 t = 0;
+    bool dense = true;   // record of the new Message-List (record-writing rounds)
+    if constexpr (LDS::kCml) {
+      if (a.cml_next) {
+        const u64x2 row = sv | nw;
+        const u64 bx = __ballot(row.x != 0ull), by = __ballot(row.y != 0ull);
+        const u64 msk = spread32((bx >> (32 * h)) & 0xFFFFFFFFull) | (spread32((by >> (32 * h)) & 0xFFFFFFFFull) << 1);
+        dense = __popcll(msk) > CML_MAXW;
+        if (!dense && on && tot) {
+          u64* rec = a.cml_next + (size_t)v * CML_WORDS;
+          const int p = 1 + __popcll(msk & ((1ull << (2 * lw)) - 1ull));
+          if (row.x) rec[p] = row.x;
+          if (row.y) rec[p + (row.x ? 1 : 0)] = row.y;
+          if (lw == 0) rec[0] = msk;
+        }
+      }
+    }
     if (on && tot) {
       alive_add<W>(a, L, lw, nw);
       store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);
@@ -815,6 +818,7 @@ __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     if (lw == 0 && on && tot) {
       L.tot[ks] = tot;
       L.dig[ks] = t;
+      if constexpr (LDS::kCml) L.cd[ks] = dense ? 1 : 0;
     }
     const uint32_t tA = (uint32_t)__builtin_amdgcn_readlane((int)tot, 0);
     const uint32_t tB = kB >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)tot, 32) : 0u;
@@ -836,8 +840,6 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, LDS& L, int
     const int v = (int)(a.vbegin + li);
     const uint32_t tot = L.tot[lane];
     a.fpop_next[v] = tot;
-    if constexpr (LDS::kCml)
-      if (a.cmk_next) a.cmk_next[v] = tot ? L.cm[lane] : 0ull;
     if (tot) {
       a.seenpop[li] += tot;
       a.sp[v] = (uint8_t)a.wslot;
@@ -847,6 +849,12 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, LDS& L, int
     }
   }
   st.add(S_NEXT_ARCS, wave_sum_u64(next_arcs));
+  if constexpr (LDS::kCml) {   // the wave's 64 vertices are one word of the dense bitmap
+    if (a.cmk_next) {
+      const u64 dm = __ballot(!need || L.tot[lane] == 0u || L.cd[lane] != 0);
+      if (lane == 0 && li < a.nloc) a.cmk_next[li >> 6] = dm;
+    }
+  }
 }
 
 // main pull kernel: a wave owns 64 consecutive vertices.  The per-vertex
@@ -929,11 +937,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         }
         L.np[lane] = (uint8_t)np;
       }
-      if (!need && !hub) {
-        a.fpop_next[v] = 0;
-        if constexpr ((MODE & SCAN_CML) != 0)
-          if (a.cmk_next) a.cmk_next[v] = 0ull;
-      }
+      if (!need && !hub) a.fpop_next[v] = 0;
       slot_of = a.sp[v];
       if (a.early_exit && need) L.mi[lane] = a.midx[v];
     }
@@ -947,7 +951,8 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     wave_sync_lds();
     const bool ee = a.early_exit != 0;
     u64 m = __ballot(need);
-    if constexpr (GP_PRE_PAIRS && W == 64 && (MODE & 3) == SCAN_PRE && (MODE & SCAN_CML) == 0) {
+    if constexpr ((MODE & SCAN_CML) != 0) L.racc[lane] = 0ull;   // record rounds: first receiver's accumulator
+    if constexpr (GP_PRE_PAIRS && W == 64 && (MODE & 3) == SCAN_PRE) {
       if (!ee) {   // prefiltered receivers two at a time, the rest below
         const u64 mp = __ballot(need && L.np[lane] != 0xFFu);
         pre_pairs<W>(a, L, mp, base, slot_of, st);
@@ -971,22 +976,22 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       if (ALIVE && ee && a.alive && !__any((want.x | want.y) != 0ull)) {
       } else if constexpr ((MODE & 3) == SCAN_PRE) {
         const uint32_t np = L.np[k];
-        bool done = false;
-        if constexpr (W == 64 && (MODE & SCAN_CML) != 0) {
-          if (np != 0xFFu && np && a.cml) {
-            stage_masks<W>(a, L, L.pre[k], (int)np, st);
-            gather_rows_cml<W>(a, L, L.pre[k], (int)np, g, lw, acc, st);
-            wave_sync_lds();
-            done = true;
-          }
-        }
-        if (done) {
-        } else if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);
+        if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
         else gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       } else {
         gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       }
       reduce_slots<W>(acc);
+      if constexpr (W == 64 && (MODE & SCAN_CML) != 0) {
+        if (a.cmk) {   // the gathered records (gather_scan ORs them into L.racc)
+          wave_sync_lds();
+          acc.x |= L.racc[2 * lw];
+          acc.y |= L.racc[2 * lw + 1];
+          wave_sync_lds();
+          L.racc[lane] = 0ull;   // for the next receiver (read by every lane above first)
+          wave_sync_lds();
+        }
+      }
       finish_row<W, true, (MODE & SCAN_CML) != 0>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot, k);
     }
     alive_flush<W>(a, L.alive, lane);
@@ -1395,10 +1400,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
     const int v = a.hubs[h];
     const int64_t i = v - a.vbegin;
     if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= a.done_at[v]) {
-      if (lane == 0) {
-        a.fpop_next[v] = 0;
-        if (a.cmk_next) a.cmk_next[v] = 0ull;
-      }
+      if (lane == 0) a.fpop_next[v] = 0;
     } else {
       st.add(S_VISITED, 1);
       u64x2 acc = {0, 0};
@@ -1838,7 +1840,7 @@ struct InjectArgs {
   uint32_t* __restrict__ fpop;
   u64* __restrict__ frx;               // exact frontier rows (track_msg_forwards, partitioned)
   int64_t frx_rows;                    // ... of vertices [0, frx_rows)
-  u64* __restrict__ cmk;               // compact-list masks of slot r & 1 (or null)
+  u64* __restrict__ cmk;               // dense bitmap of slot r & 1 (record rounds, or null)
   u64* __restrict__ alive;             // [W] alive messages of round r (or null)
   uint32_t* __restrict__ seenpop;
   uint8_t* __restrict__ first;
@@ -1882,7 +1884,7 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
         a.slot[a.rslot][(size_t)o * a.words + lane] = s | b;
         if (has_frx) a.frx[(size_t)o * a.words + lane] = f | b;
       }
-      if (a.cmk && lane == 0) a.cmk[o] = CML_DENSE;   // a sender this round, read as a full row
+      if (a.cmk && lane == 0) set_dense(a.cmk, o);   // a sender this round: its record (if any) is stale
       if (a.alive && b) atomicOr(a.alive + lane, b);   // injected messages are forwarded this round
       const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
       if (lane == 0) {
@@ -2426,16 +2428,17 @@ static int launch_expand(Ctx* c) {
     c->sum_now = true;
   }
 #endif
-  // compact Message-Lists (W = 64): written while the rows are sparse (last
+  // Message-List records (W = 64): written while the rows are sparse (last
   // round's receivers got <= CML_AVG_BITS new bits on average), read by a
-  // filtered pull whose senders all wrote theirs in the previous round
+  // filtered pull without early exit whose senders all wrote theirs (or their
+  // dense bit) in the previous round.  Senders are exactly the vertices with
+  // fpop != 0 under liveness too (a crash zeroes fpop), and a sender's record
+  // mirrors its row, so records and full rows give the same OR.
   {
     constexpr double CML_AVG_BITS = 16.0;
     const bool ok = c->d_cml[0] != nullptr && c->words == 64 && !c->mode_push;
     const bool sparse = (double)c->prev_new_bits <= CML_AVG_BITS * (double)std::max<u64>(c->prev_receivers, 1);
-    // (not with liveness: a crash zeroes fpop, not the mask word)
-    c->cml_read_now = ok && sparse && c->cml_written_prev && !c->unfiltered_now && !c->arc_mask_now &&
-                      !c->liveness_active;
+    c->cml_read_now = ok && c->cml_written_prev && !c->unfiltered_now && !c->arc_mask_now && !c->early_exit_now;
     c->cml_write_now = ok && sparse && !c->unfiltered_now && !c->arc_mask_now;   // the kernels that write them
   }
   // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
@@ -2665,8 +2668,8 @@ static int alloc_state(Ctx* c) {
   if (c->cfg.compact_rows && W == 64 && c->nranks == 1) {
     GP_TRY(dalloc(&c->d_cml[0], na * CML_WORDS));
     GP_TRY(dalloc(&c->d_cml[1], na * CML_WORDS));
-    GP_TRY(dalloc(&c->d_cmk[0], na));
-    GP_TRY(dalloc(&c->d_cmk[1], na));
+    GP_TRY(dalloc(&c->d_cmk[0], (na + 63) / 64));   // dense bitmaps
+    GP_TRY(dalloc(&c->d_cmk[1], (na + 63) / 64));
   } else {
     dfree(&c->d_cml[0]);
     dfree(&c->d_cml[1]);

@@ -151,7 +151,7 @@ struct Ctx {
   bool prefilter_now = false;       // this round's filtered pull probes low-degree in-lists lane-parallel
   // compact Message-Lists: 128-B records per vertex, per slot
   u64* d_cml[2] = {nullptr, nullptr};   // [n_alloc][16] records
-  u64* d_cmk[2] = {nullptr, nullptr};   // [n_alloc] masks (0: not a sender)
+  u64* d_cmk[2] = {nullptr, nullptr};   // [n_alloc / 64] dense bitmaps (bit v: no record, read the row)
   bool cml_read_now = false, cml_write_now = false, cml_written_prev = false;
   int64_t inj_groups_at(int32_t r) const {
     auto it = inject.find(r);
