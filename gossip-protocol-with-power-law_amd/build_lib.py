@@ -49,7 +49,7 @@ def build(force=False, verbose=True):
         if p.wait() != 0:
             raise RuntimeError("hipcc failed")
     tmp = LIB + ".tmp"
-    cmd = [_hipcc(), *FLAGS, "-shared", *objs, "-o", tmp, "-lrccl"]
+    cmd = [_hipcc(), *FLAGS, "-shared", *objs, "-o", tmp, "-lrccl", "-pthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)

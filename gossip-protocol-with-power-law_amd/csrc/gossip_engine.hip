@@ -266,6 +266,7 @@ template <bool PRE, bool CML>
 struct WaveLdsT {
   static constexpr bool kPre = PRE, kCml = CML;
   u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
+  u64 seen2[64];        // pair paths: the second receiver's seen row
   int32_t idx[64];      // active neighbours of one pass
   uint32_t tot[64];     // k_expand: new bits of the wave's vertex k (committed after the loop)
   u64 dig[64];          // k_expand: digest terms of vertex k
@@ -725,15 +726,92 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   st.add(S_WRITTEN, 1);
 }
 
-// SCAN_PRE rounds without early exit (round 1 of a C4 run: 7.9 M receivers,
-// about 2 active in-neighbours each, already found by the lane phase): two
-// receivers per wave, one per half.  A half-wave loads a whole 64-word row per
-// instruction, so each receiver keeps its rows in flight on its own and the
-// chain rows -> commit is walked for two receivers at a time.  Same commits
-// as finish_row (deferred per-vertex words in L.tot / L.dig).
+// Receivers two at a time, one per half-wave (W = 64).  A half-wave loads a
+// whole 64-word row per instruction, so each receiver keeps its rows in flight
+// on its own and the dependent chain (column ids -> probes -> rows -> commit)
+// is walked for two receivers at once: the latency-bound rounds' lever, since
+// 64 VGPRs already give the 8 waves per SIMD the hardware holds.  Same
+// commits as finish_row (deferred per-vertex words in L.tot / L.dig / L.cd).
 #ifndef GP_PRE_PAIRS
 #define GP_PRE_PAIRS 1
 #endif
+#ifndef GP_SHORT_PAIRS
+#define GP_SHORT_PAIRS 0
+#endif
+constexpr int SHORT_DEG = 32;   // in-degree up to which a receiver's arcs fit one half-wave pass
+
+// receiver side of a pair: half h holds receiver ks (on: the half has one;
+// kB < 0: half 1 idle) with its gathered OR acc and its seen row sv
+template <int W, class LDS>
+__device__ __forceinline__ void pair_finish(const ExpandArgs& a, LDS& L, int h, int lw, bool on, int ks, int kB,
+                                            int64_t i, int v, u64x2 acc, u64x2 sv, WaveStats& st) {
+  const u64x2 nw = acc & ~sv;
+  uint32_t tot = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
+  u64 t = 0;
+  bool dense = true;   // record of the new Message-List (record-writing rounds)
+  if constexpr (LDS::kCml) {
+    if (a.cml_next) {
+      const u64x2 row = sv | nw;
+      const u64 bx = __ballot(row.x != 0ull), by = __ballot(row.y != 0ull);
+      const u64 msk = spread32((bx >> (32 * h)) & 0xFFFFFFFFull) | (spread32((by >> (32 * h)) & 0xFFFFFFFFull) << 1);
+      dense = __popcll(msk) > CML_MAXW;
+      if (!dense && on && tot) {
+        u64* rec = a.cml_next + (size_t)v * CML_WORDS;
+        const int p = 1 + __popcll(msk & ((1ull << (2 * lw)) - 1ull));
+        if (row.x) rec[p] = row.x;
+        if (row.y) rec[p + (row.x ? 1 : 0)] = row.y;
+        if (lw == 0) rec[0] = msk;
+      }
+    }
+  }
+  if (on && tot) {
+    alive_add<W>(a, L, lw, nw);
+    store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);
+    if (a.frx_next) store_piece<W>(a.frx_next, v, lw, nw);
+    if (a.first) {
+      uint8_t* row = a.first + (size_t)i * (W * 64);
+      if (nw.x) set_first_bytes(row, 2 * lw, nw.x, (uint32_t)a.rr);
+      if (nw.y) set_first_bytes(row, 2 * lw + 1, nw.y, (uint32_t)a.rr);
+    }
+    if (a.digest) {
+      if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 2 * lw), nw.x);
+      if (nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 2 * lw + 1), nw.y);
+    }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) t ^= __shfl_xor(t, o);
+  if (lw == 0 && on && tot) {
+    L.tot[ks] = tot;
+    L.dig[ks] = t;
+    if constexpr (LDS::kCml) L.cd[ks] = dense ? 1 : 0;
+  }
+  const uint32_t tA = (uint32_t)__builtin_amdgcn_readlane((int)tot, 0);
+  const uint32_t tB = kB >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)tot, 32) : 0u;
+  st.add(S_NEW_BITS, (u64)tA + (u64)tB);
+  st.add(S_RECEIVERS, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
+  st.add(S_WRITTEN, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
+}
+
+// the seen row of a pair's receivers, loaded after a gather without early
+// exit (only by a half that gathered something), and its S_SEEN_READ count
+template <int W>
+__device__ __forceinline__ u64x2 pair_seen(const ExpandArgs& a, int h, int lw, bool on, int kB, int v,
+                                           uint32_t sv_slot, u64x2 acc, WaveStats& st) {
+  const u64 bz = __ballot(on && (acc.x | acc.y) != 0ull);
+  const bool any_h = ((bz >> (32 * h)) & 0xFFFFFFFFull) != 0ull;
+  u64x2 sv = {0, 0};
+  if (any_h && sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
+  const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
+  const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
+  st.add(S_SEEN_READ, (u64)(((bz & 0xFFFFFFFFull) && sA != SLOT_NONE) ? 1 : 0) +
+                          (u64)(((bz >> 32) && kB >= 0 && sB != SLOT_NONE) ? 1 : 0));
+  return sv;
+}
+
+// SCAN_PRE rounds without early exit (round 1 of a C4 run: 7.9 M receivers,
+// about 2 active in-neighbours each, already found by the lane phase)
 template <int W, class LDS>
 __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
                                           WaveStats& st) {
@@ -768,64 +846,106 @@ __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     }
     st.add(S_GATHERED, (u64)(npA + npB));
     st.add(S_ROW_BYTES, (u64)(npA + npB) * (u64)(8 * W));
-    const u64 bz = __ballot(on && (acc.x | acc.y) != 0ull);
-    const bool any_h = ((bz >> (32 * h)) & 0xFFFFFFFFull) != 0ull;
-    u64x2 sv = {0, 0};
-    if (any_h && sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
-    {
+    const u64x2 sv = pair_seen<W>(a, h, lw, on, kB, v, sv_slot, acc, st);
+    pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, acc, sv, st);
+  }
+}
+
+// receivers with at most SHORT_DEG in-arcs, any pull mode but the per-arc
+// mask: each half-wave loads its receiver's column ids in one pass, probes
+// them, stages the active ones in its half of L.idx and gathers them; early
+// exit (target, word skip, stop) runs per half, the seen row stays in
+// registers
+template <int W, int MODE, bool ALIVE, int RIF, class LDS>
+__device__ __forceinline__ void short_pairs_n(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
+                                              WaveStats& st, bool ee) {
+  static_assert(W == 64, "half-wave rows");
+  const int lane = threadIdx.x & 63, h = lane >> 5, lw = lane & 31;
+  while (mp) {
+    const int kA = __ffsll((long long)mp) - 1;
+    mp &= mp - 1;
+    int kB = -1;
+    if (mp) {
+      kB = __ffsll((long long)mp) - 1;
+      mp &= mp - 1;
+    }
+    const bool on = h == 0 || kB >= 0;
+    const int ks = (h && kB >= 0) ? kB : kA;
+    const int64_t i = base + ks;
+    const int v = (int)(a.vbegin + i);
+    const int64_t vb = L.rp[ks];
+    const int deg = on ? (int)(L.rp[ks + 1] - vb) : 0;
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
+    u64x2 want = {0, 0};
+    u64* const pseen = h ? L.seen2 : L.seen;   // early exit: this half's seen row, parked for the commit
+    if (ee) {
       const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
       const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
-      st.add(S_SEEN_READ, (u64)(((bz & 0xFFFFFFFFull) && sA != SLOT_NONE) ? 1 : 0) +
-                              (u64)(((bz >> 32) && kB >= 0 && sB != SLOT_NONE) ? 1 : 0));
+      st.add(S_SEEN_READ, (u64)((sA != SLOT_NONE ? 1 : 0) + (kB >= 0 && sB != SLOT_NONE ? 1 : 0)));
+      u64x2 sv = {0, 0};
+      if (on) {
+        if (sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
+        u64x2 cm = load_piece<W>(a.cmask, L.mi[ks], lw);
+        if (ALIVE && a.alive) cm &= load_piece<W>(a.alive, 0, lw);
+        want = cm & ~sv;
+      }
+      pseen[2 * lw] = sv.x;
+      pseen[2 * lw + 1] = sv.y;
     }
-    const u64x2 nw = acc & ~sv;
-    uint32_t tot = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
+    int32_t ent = -1;
+    if (lw < deg) ent = probe<MODE>(a, a.gcol[vb + lw]);
+    if (ALIVE && ee && a.alive) {   // a half holding every alive message of its component scans nothing
+      const u64 wb = __ballot((want.x | want.y) != 0ull);
+      if (((wb >> (32 * h)) & 0xFFFFFFFFull) == 0ull) ent = -1;
+    }
+    const u64 bm = __ballot(ent >= 0);
+    if (ent >= 0) L.idx[32 * h + __popcll(bm & (((1ull << lw) - 1ull) << (32 * h)))] = ent;
+    wave_sync_lds();
+    const int cntA = __popcll(bm & 0xFFFFFFFFull), cntB = __popcll(bm >> 32);
+    const int cnt = h ? cntB : cntA;
+    st.add(S_ARCS, (u64)((uint32_t)__builtin_amdgcn_readlane(deg, 0) + (uint32_t)__builtin_amdgcn_readlane(deg, 32)));
+    u64x2 acc = {0, 0};
+    bool live = true;   // this lane's words still miss messages (word skip)
+    if (GP_WORD_SKIP && ee) live = (want.x | want.y) != 0ull;
+    const int nmax = max(cntA, cntB);
+    for (int k0 = 0; k0 < nmax; k0 += RIF) {
+      u64x2 r[RIF];
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
-    u64 t = 0;
-    bool dense = true;   // record of the new Message-List (record-writing rounds)
-    if constexpr (LDS::kCml) {
-      if (a.cml_next) {
-        const u64x2 row = sv | nw;
-        const u64 bx = __ballot(row.x != 0ull), by = __ballot(row.y != 0ull);
-        const u64 msk = spread32((bx >> (32 * h)) & 0xFFFFFFFFull) | (spread32((by >> (32 * h)) & 0xFFFFFFFFull) << 1);
-        dense = __popcll(msk) > CML_MAXW;
-        if (!dense && on && tot) {
-          u64* rec = a.cml_next + (size_t)v * CML_WORDS;
-          const int p = 1 + __popcll(msk & ((1ull << (2 * lw)) - 1ull));
-          if (row.x) rec[p] = row.x;
-          if (row.y) rec[p + (row.x ? 1 : 0)] = row.y;
-          if (lw == 0) rec[0] = msk;
-        }
+      for (int q = 0; q < RIF; ++q) {
+        r[q] = u64x2{0, 0};
+        if (k0 + q < cnt && live) r[q] = load_piece<W>(a.rows, L.idx[32 * h + k0 + q], lw);
       }
-    }
-    if (on && tot) {
-      alive_add<W>(a, L, lw, nw);
-      store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);
-      if (a.frx_next) store_piece<W>(a.frx_next, v, lw, nw);
-      if (a.first) {
-        uint8_t* row = a.first + (size_t)i * (W * 64);
-        if (nw.x) set_first_bytes(row, 2 * lw, nw.x, (uint32_t)a.rr);
-        if (nw.y) set_first_bytes(row, 2 * lw + 1, nw.y, (uint32_t)a.rr);
-      }
-      if (a.digest) {
-        if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 2 * lw), nw.x);
-        if (nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 2 * lw + 1), nw.y);
-      }
-    }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) t ^= __shfl_xor(t, o);
-    if (lw == 0 && on && tot) {
-      L.tot[ks] = tot;
-      L.dig[ks] = t;
-      if constexpr (LDS::kCml) L.cd[ks] = dense ? 1 : 0;
+      for (int q = 0; q < RIF; ++q) acc |= r[q];
+      uint32_t pieces = 0;
+#pragma unroll
+      for (int q = 0; q < RIF; ++q) pieces += (uint32_t)__popcll(__ballot(k0 + q < cnt && live));
+      st.add(S_ROW_BYTES, (u64)pieces * (u64)(8 * Geo<W>::WPL));
+      st.add(S_GATHERED, (u64)(min(RIF, max(cntA - k0, 0)) + min(RIF, max(cntB - k0, 0))));
+      if (ee) {
+        const u64x2 miss = want & ~acc;
+        live = (miss.x | miss.y) != 0ull;
+        if (!__any(live)) break;
+      }
     }
-    const uint32_t tA = (uint32_t)__builtin_amdgcn_readlane((int)tot, 0);
-    const uint32_t tB = kB >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)tot, 32) : 0u;
-    st.add(S_NEW_BITS, (u64)tA + (u64)tB);
-    st.add(S_RECEIVERS, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
-    st.add(S_WRITTEN, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
+    wave_sync_lds();   // L.idx is restaged by the next pair
+    u64x2 sv;
+    if (ee) {
+      sv.x = pseen[2 * lw];
+      sv.y = pseen[2 * lw + 1];
+    } else {
+      sv = pair_seen<W>(a, h, lw, on, kB, v, sv_slot, acc, st);
+    }
+    pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, acc, sv, st);
   }
+}
+template <int W, int MODE, bool ALIVE, class LDS>
+__device__ __forceinline__ void short_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
+                                            WaveStats& st, bool ee) {
+  if (GP_ROWS_IN_FLIGHT > GP_NEAR_DONE_RIF && a.near_done)
+    short_pairs_n<W, MODE, ALIVE, GP_NEAR_DONE_RIF>(a, L, mp, base, slot_of, st, ee);
+  else
+    short_pairs_n<W, MODE, ALIVE, GP_ROWS_IN_FLIGHT>(a, L, mp, base, slot_of, st, ee);
 }
 
 // k_expand's commit of the deferred per-vertex words: lane k holds vertex
@@ -957,6 +1077,15 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         const u64 mp = __ballot(need && L.np[lane] != 0xFFu);
         pre_pairs<W>(a, L, mp, base, slot_of, st);
         m &= ~mp;
+      }
+    }
+    if constexpr (GP_SHORT_PAIRS && W == 64 && (MODE & 3) != SCAN_MASKED) {
+      bool pairs = true;   // (record rounds read records in the single-receiver scan)
+      if constexpr ((MODE & SCAN_CML) != 0) pairs = a.cmk == nullptr;
+      if (pairs) {   // receivers with short in-lists two at a time, the rest below
+        const u64 msp = m & __ballot(need && L.rp[lane + 1] - L.rp[lane] <= SHORT_DEG);
+        short_pairs<W, SCAN, ALIVE>(a, L, msp, base, slot_of, st, ee);
+        m &= ~msp;
       }
     }
     while (m) {

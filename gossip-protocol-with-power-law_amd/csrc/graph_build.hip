@@ -19,7 +19,9 @@
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
 
+#include <algorithm>
 #include <cmath>
+#include <thread>
 #include <vector>
 
 #include "gp_internal.h"
@@ -39,14 +41,28 @@ struct AliasTable {
 static void build_alias(int64_t n, double gamma, AliasTable& t) {
   const double alpha = 1.0 / (gamma - 1.0);
   std::vector<uint64_t> q((size_t)n);
-  uint64_t T = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    double w = std::ldexp(std::pow((double)(i + 1), -alpha), 32);
-    uint64_t qi = (uint64_t)std::floor(w);
-    if (qi < 1) qi = 1;
-    q[(size_t)i] = qi;
-    T += qi;
+  // the weights in parallel (one pow per vertex: most of a 2^24 build's host
+  // time); integer sums, so the total is the same in any order
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(16, n >> 16));
+  std::vector<uint64_t> part((size_t)nt, 0);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nt; ++t) {
+    pool.emplace_back([&, t]() {
+      const int64_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+      uint64_t sum = 0;
+      for (int64_t i = i0; i < i1; ++i) {
+        const double w = std::ldexp(std::pow((double)(i + 1), -alpha), 32);
+        uint64_t qi = (uint64_t)std::floor(w);
+        if (qi < 1) qi = 1;
+        q[(size_t)i] = qi;
+        sum += qi;
+      }
+      part[(size_t)t] = sum;
+    });
   }
+  for (auto& th : pool) th.join();
+  uint64_t T = 0;
+  for (uint64_t x : part) T += x;
   t.total = T;
   t.prob.assign((size_t)n, T);
   t.alias.resize((size_t)n);

@@ -13,6 +13,6 @@ F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result --offload-arch=gfx950 $2"
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/partition.hip -o $OUT/pt.o &
 /opt/rocm/bin/hipcc $F -c $PKG/csrc/bitcount.hip -o $OUT/bc.o &
 wait
-/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o $OUT/ck.o $OUT/pt.o $OUT/bc.o -o $PKG/_ab/$1.so -lrccl
+/opt/rocm/bin/hipcc $F -shared $OUT/ge.o $OUT/gb.o $OUT/ck.o $OUT/pt.o $OUT/bc.o -o $PKG/_ab/$1.so -lrccl -pthread
 rm -rf $OUT
 echo $PKG/_ab/$1.so
