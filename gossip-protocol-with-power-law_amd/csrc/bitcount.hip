@@ -31,7 +31,7 @@ constexpr int BC_MAXCNT = 2047;   // what ones/twos/fours + 8 planes of eights c
 constexpr uint8_t BC_SLOT_NONE = 0xFF;
 
 struct BitcountArgs {
-  const u64* slot[2];               // Message-List slots; row v = slot[sp[v]][v] (sp 0xFF: empty)
+  const u64* slot[3];               // Message-List slots; row v = slot[sp[v]][v] (sp 0xFF: empty; 2: parked)
   const uint8_t* __restrict__ sp;
   const u64* __restrict__ keys;     // [count] sorted (deg << 32 | v), or null: position = vertex, unweighted
   int64_t count;
@@ -329,6 +329,7 @@ int bitcount_messages(Ctx* c, bool weighted, u64* cov, u64* fwd) {
   BitcountArgs a{};
   a.slot[0] = c->d_slot[0];
   a.slot[1] = c->d_slot[1];
+  a.slot[2] = c->d_slot[2];
   a.sp = c->d_sp;
   a.keys = weighted ? c->d_bc_keys : nullptr;
   a.count = n;
@@ -508,6 +509,7 @@ int finalize_by_components(Ctx* c, bool weighted, u64* cov, u64* fwd) {
   BitcountArgs a{};
   a.slot[0] = c->d_slot[0];
   a.slot[1] = c->d_slot[1];
+  a.slot[2] = c->d_slot[2];
   a.sp = c->d_sp;
   a.keys = c->d_fin_list;
   a.count = n;

@@ -77,7 +77,7 @@ static int64_t blob_bytes(Ctx* c, int64_t nrep) {
 }
 
 // rows[t] = word t % W of vertex v0 + t / W's Message-List row (zero if none)
-__global__ void k_ckpt_gather(const u64* __restrict__ s0, const u64* __restrict__ s1,
+__global__ void k_ckpt_gather(const u64* __restrict__ s0, const u64* __restrict__ s1, const u64* __restrict__ s2,
                               const uint8_t* __restrict__ sp, u64* __restrict__ out, int64_t v0,
                               int64_t words_total, int32_t W) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -85,7 +85,7 @@ __global__ void k_ckpt_gather(const u64* __restrict__ s0, const u64* __restrict_
   const int64_t v = v0 + t / W;
   const uint8_t p = sp[v];
   const size_t i = (size_t)v * W + (size_t)(t % W);
-  out[t] = p == CK_SLOT_NONE ? 0ull : (p == 0 ? s0[i] : s1[i]);
+  out[t] = p == CK_SLOT_NONE ? 0ull : (p == 0 ? s0[i] : p == 1 ? s1[i] : s2[i]);   // 2: parked
 }
 __global__ void k_ckpt_scatter(u64* __restrict__ slot, const u64* __restrict__ in, int64_t v0,
                                int64_t words_total, int32_t W) {
@@ -143,7 +143,7 @@ int gp_checkpoint_save(gp_ctx* c, void* host, int64_t bytes) {
   for (int64_t t0 = 0; t0 < total; t0 += chunk) {
     const int64_t cnt = std::min(chunk, total - t0);
     hipLaunchKernelGGL(k_ckpt_gather, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, c->stream, c->d_slot[0],
-                       c->d_slot[1], c->d_sp, stage, t0 / W, cnt, (int32_t)W);
+                       c->d_slot[1], c->d_slot[2], c->d_sp, stage, t0 / W, cnt, (int32_t)W);
     hipError_t e = hipGetLastError();
     int rc = e == hipSuccess ? copy_sync(c, out + off + t0 * 8, stage, (size_t)cnt * 8, hipMemcpyDeviceToHost)
                              : set_error(GP_EHIP, std::string("k_ckpt_gather: ") + hipGetErrorString(e));

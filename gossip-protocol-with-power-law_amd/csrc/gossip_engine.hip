@@ -223,6 +223,7 @@ struct ExpandArgs {
 };
 
 constexpr uint8_t SLOT_NONE = 0xFF;
+constexpr uint8_t SLOT_PARKED = 2;   // row in d_slot[2] (a down vertex, before an unfiltered pull)
 
 // Message-List records (W = 64): a round whose receivers end
 // up with sparse Message-Lists also writes, per receiver, a 128-B record --
@@ -1832,6 +1833,36 @@ __global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64* __restrict__ ab
   }
 }
 
+// Parking (before an unfiltered pull under liveness): a down vertex's row may
+// hold bits it never sent (it crashed with them) and the unfiltered pull would
+// forward them, so its row moves to slot 2 and both read-slot rows are zeroed.
+// One wave per 64 vertices; rows stay parked for the rest of the run.
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_park(const uint8_t* __restrict__ state, uint8_t* __restrict__ sp,
+                                                u64* __restrict__ s0, u64* __restrict__ s1, u64* __restrict__ s2,
+                                                int64_t n_alloc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (w * 64 >= n_alloc) return;
+  const int64_t v0 = w * 64 + lane;
+  uint32_t p = SLOT_NONE;
+  if (v0 < n_alloc && (state[v0] & ST_DOWN)) p = sp[v0];
+  const bool move = p < 2u;
+  u64 todo = __ballot(move);
+  if (move) sp[v0] = SLOT_PARKED;
+  while (todo) {
+    const int b = __ffsll((long long)todo) - 1;
+    todo &= todo - 1;
+    const uint32_t q = (uint32_t)__shfl((int)p, b);
+    if (lane < W) {
+      const size_t i = (size_t)(w * 64 + b) * W + lane;
+      s2[i] = (q ? s1 : s0)[i];
+      s0[i] = 0ull;
+      s1[i] = 0ull;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // weakly connected components (union-find, hook larger root under smaller,
 // so the label of a component is its smallest vertex id).  A vertex holding
@@ -2265,10 +2296,8 @@ __global__ __launch_bounds__(BLOCK) void k_detect(LiveArgs a) {
 // over rows [0, count).  Lane l holds word l % W of vertex slot l / W; each lane
 // keeps 64 register counters per output.
 struct BitsumArgs {
-  const u64* __restrict__ rows;       // [count][W] (when sel is null)
+  const u64* __restrict__ rows;       // [count][W]
   const uint32_t* __restrict__ guard; // optional: row valid iff guard[i] != 0
-  const u64* slot[2];                 // with sel: row i is slot[sel[i]][i] (SLOT_NONE: zero)
-  const uint8_t* __restrict__ sel;
   const int32_t* __restrict__ weight; // [count]
   u64* __restrict__ cnt;              // [W*64] or null
   u64* __restrict__ wsum;             // [W*64] or null
@@ -2297,10 +2326,7 @@ __global__ __launch_bounds__(BLOCK) void k_bitsum(BitsumArgs a) {
   const int64_t step = (int64_t)gridDim.x * WAVES * VPS;
   for (int64_t i = ((int64_t)blockIdx.x * WAVES + wib) * VPS + q; i < a.count; i += step) {
     u64 x = 0;
-    if (a.sel) {
-      const uint32_t p = a.sel[i];
-      if (p != SLOT_NONE) x = a.slot[p][i * W + w];
-    } else if (!a.guard || a.guard[i] != 0) {
+    if (!a.guard || a.guard[i] != 0) {
       x = a.rows[i * W + w];
     }
     const uint32_t wt = SUM ? (uint32_t)max(a.weight[i], 0) : 0u;
@@ -2430,6 +2456,9 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     return;
   }
   const int64_t per_block = (int64_t)WAVES * 64;
+  if (a.unfiltered && c->liveness_active)
+    hipLaunchKernelGGL(k_park<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
+                       c->d_state, c->d_sp, c->d_slot[0], c->d_slot[1], c->d_slot[2], c->n_alloc);
   if (a.unfiltered)
     hipLaunchKernelGGL(k_fixup_rows<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
                        c->d_abits, c->d_ws, c->d_slot[c->cur], c->cur, c->n_alloc);
@@ -2468,7 +2497,12 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     }
   } else if (a.nloc > 0) {
     const dim3 grid(grid_for(a.nloc, per_block));
-    if (mode == SCAN_UNFILTERED)
+    bool alive_ee = false;   // unfiltered under liveness (parked rows) with early exit
+    if constexpr (W >= 32) alive_ee = mode == SCAN_UNFILTERED && a.alive && a.early_exit;
+    if (alive_ee) {
+      if constexpr (W >= 32)
+        hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
+    } else if (mode == SCAN_UNFILTERED)
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
     else if (masked)
       hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(BLOCK), 0, c->stream, a);
@@ -2514,6 +2548,9 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   }
 }
 
+#ifndef GP_PARK
+#define GP_PARK 1
+#endif
 static int launch_expand(Ctx* c) {
   if (alive_on(c))   // F_{r+1} is built by this round's receivers
     GP_HIP(hipMemsetAsync(c->d_alive + (size_t)(c->cur ^ 1) * c->words, 0, (size_t)c->words * 8, c->stream));
@@ -2535,11 +2572,24 @@ static int launch_expand(Ctx* c) {
   if (c->mode_push && c->nloc() > 0)
     GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1], 0, (size_t)c->nloc() * 4, c->stream));
   // unfiltered pull when (nearly) every vertex is a sender: last round's
-  // receivers + this round's injected origins >= unfiltered_pct % of n.  Not
-  // with liveness: a crashed vertex's Message-List may hold bits it never sent.
+  // receivers + this round's injected origins >= unfiltered_pct % of n.  With
+  // liveness a crashed vertex's Message-List may hold bits it never sent, so
+  // the down vertices' rows are parked first (k_park; one vertex set per
+  // context, hence not in a vertex partition, whose ghosts' rows are frontiers)
   const double senders = (double)c->prev_receivers + (double)c->inj_groups_at(r);
-  c->unfiltered_now = !c->mode_push && c->cfg.unfiltered_pct > 0 && !c->liveness_active &&
+  c->unfiltered_now = !c->mode_push && c->cfg.unfiltered_pct > 0 &&
                       senders * 100.0 >= (double)c->cfg.unfiltered_pct * (double)c->n;
+  if (c->unfiltered_now && c->liveness_active) {
+    if (c->local || c->park_failed || !GP_PARK) {
+      c->unfiltered_now = false;
+    } else if (!c->d_slot[2]) {
+      if (dalloc(&c->d_slot[2], (size_t)c->n_alloc * c->words) != 0) {
+        c->park_failed = true;   // (out of memory: stay filtered)
+        c->unfiltered_now = false;
+        (void)hipGetLastError();
+      }
+    }
+  }
   // filtered pull: probe every arc inside the scan, or build the per-arc mask
   // first (pays once the probes are many: senders >= arc_mask_permille of n)
   c->arc_mask_now = !c->mode_push && !c->unfiltered_now && c->cfg.arc_mask_permille > 0 &&
@@ -2680,6 +2730,8 @@ static int set_partition(Ctx* c, int32_t rank, int32_t nranks) {
 }
 
 static void free_state(Ctx* c) {
+  dfree(&c->d_slot[2]);
+  c->park_failed = false;
   for (int k = 0; k < 2; ++k) {
     dfree(&c->d_slot[k]);
     dfree(&c->d_frx[k]);
@@ -2773,6 +2825,8 @@ static int alloc_state(Ctx* c) {
   // partition, which sends owned vertices' new bits: the owned rows only (a
   // ghost's slot row is its frontier)
   c->frx_rows = c->local ? c->nloc() : (c->cfg.track_msg_forwards ? c->n_alloc : 0);
+  dfree(&c->d_slot[2]);   // (re)allocated at the first parking, for this W
+  c->park_failed = false;
   for (int k = 0; k < 2; ++k) {
     GP_TRY(dalloc(&c->d_slot[k], na * W));
     GP_TRY(dalloc(&c->d_fpop[k], na));
@@ -2977,6 +3031,7 @@ void gp_destroy(gp_ctx* c) {
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
+  dfree(&c->d_slot[2]);
   for (int k = 0; k < 2; ++k) { dfree(&c->d_slot[k]); dfree(&c->d_frx[k]); dfree(&c->d_fpop[k]); }
   dfree(&c->d_sp); dfree(&c->d_ws);
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
@@ -3560,16 +3615,19 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
     case GP_SEEN:
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(nl * W * 8));
-      if (bytes) {   // owned rows of both slots, picked per vertex by its slot byte
-        std::vector<uint64_t> s1((size_t)(nl * W));
+      if (bytes) {   // owned rows of every slot, picked per vertex by its slot byte
+        std::vector<uint64_t> s1((size_t)(nl * W)), s2(c->d_slot[2] ? (size_t)(nl * W) : 0);
         std::vector<uint8_t> sp((size_t)nl);
         GP_TRY(copy_sync(c, host, c->d_slot[0], (size_t)bytes, hipMemcpyDeviceToHost));
         GP_TRY(copy_sync(c, s1.data(), c->d_slot[1], (size_t)bytes, hipMemcpyDeviceToHost));
+        if (c->d_slot[2]) GP_TRY(copy_sync(c, s2.data(), c->d_slot[2], (size_t)bytes, hipMemcpyDeviceToHost));
         GP_TRY(copy_sync(c, sp.data(), c->d_sp, (size_t)nl, hipMemcpyDeviceToHost));
         uint64_t* h = static_cast<uint64_t*>(host);
         for (int64_t v = 0; v < nl; ++v) {
-          if (sp[(size_t)v] == SLOT_NONE) std::memset(h + v * W, 0, (size_t)W * 8);
-          else if (sp[(size_t)v] == 1) std::memcpy(h + v * W, s1.data() + v * W, (size_t)W * 8);
+          const uint8_t p = sp[(size_t)v];
+          if (p == SLOT_NONE) std::memset(h + v * W, 0, (size_t)W * 8);
+          else if (p == 1) std::memcpy(h + v * W, s1.data() + v * W, (size_t)W * 8);
+          else if (p == SLOT_PARKED && !s2.empty()) std::memcpy(h + v * W, s2.data() + v * W, (size_t)W * 8);
         }
       }
       return 0;

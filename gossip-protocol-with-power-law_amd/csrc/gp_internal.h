@@ -113,7 +113,11 @@ struct Ctx {
   // per-run state
   // Message-List slots: v's seen row lives in d_slot[d_sp[v]];
   // round r reads S[r & 1] and writes S[(r + 1) & 1]; cur == r & 1
-  u64* d_slot[2] = {nullptr, nullptr};    // [n_alloc][W]
+  u64* d_slot[3] = {nullptr, nullptr, nullptr};    // [n_alloc][W]; slot 2: parked rows (below)
+  // parking: an unfiltered pull under liveness reads every in-neighbour's row
+  // of slot r & 1, so before it the rows of down vertices move to slot 2
+  // (sp = 2) and both read-slot rows are zeroed; slot 2 is allocated lazily
+  bool park_failed = false;         // slot 2 could not be allocated: no unfiltered pull under liveness
   uint8_t* d_sp = nullptr;          // [n_alloc] slot of v's seen row (0xFF: none)
   uint8_t* d_ws = nullptr;          // [n_alloc] bit p: slot p written this run
   u64* d_frx[2] = {nullptr, nullptr};     // exact frontier rows (track_msg_forwards; partitioned)

@@ -151,6 +151,24 @@ def test_churn_random(pkg, oracle, mode):
     r["eng"].close()
 
 
+@pytest.mark.parametrize("n,m,p_fail", [(5000, 128, 0.03), (3000, 1000, 0.02), (1500, 4096, 0.05)])
+@pytest.mark.parametrize("flat_max_words", [0, 16])
+def test_unfiltered_pull_parks_crashed_rows(pkg, oracle, n, m, p_fail, flat_max_words):
+    """Unfiltered pull under churn: before each unfiltered round the rows of the
+    down vertices move to the parked slot (k_park), so no receiver ORs in bits a
+    crashed vertex never sent; seen rows, coverage (finalize reads parked rows)
+    and reports match the oracle."""
+    g = pkg.overlay.barabasi_albert(n, 3, seed=n)
+    origin = pkg.overlay.random_origins(g.n, m, seed=m)
+    inject = (np.arange(m) % 4).astype(np.int32)
+    r = _compare(pkg, oracle, g, origin, inject, crashes=[(int(origin[0]), 2), (int(origin[1]), 3)],
+                 churn=True, p_fail=p_fail, churn_seed=31, push_ratio=0.0, unfiltered_pct=1,
+                 flat_max_words=flat_max_words, arc_mask_permille=0)
+    assert sum(1 for s in r["stats"] if s["scan"] & 3 == 2) >= 3, [s["scan"] for s in r["stats"]]
+    assert sum(s["crashed"] for s in r["stats"]) > 0
+    r["eng"].close()
+
+
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_explicit_crashes_directed(pkg, oracle, mode):
     push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
@@ -429,7 +447,8 @@ def test_wide_rows_churn(pkg, oracle, mode):
     churn = dict(churn=True, p_fail=0.01, churn_seed=5)
     r = _compare(pkg, oracle, g, origin, inject, first=cfg_first, hub_threshold=512, push_ratio=push_ratio,
                  unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask, **churn)
-    assert not any(s["scan"] == 2 for s in r["stats"])   # never unfiltered with liveness
+    if push_ratio == 0.0:   # unfiltered under liveness: crashed rows parked first
+        assert any(s["scan"] == 2 for s in r["stats"]) == (unfiltered_pct == 1)
     r["eng"].close()
 
 
