@@ -739,6 +739,9 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
 #ifndef GP_SHORT_PAIRS
 #define GP_SHORT_PAIRS 0
 #endif
+#ifndef GP_PAIR_RIF
+#define GP_PAIR_RIF GP_ROWS_IN_FLIGHT
+#endif
 constexpr int SHORT_DEG = 32;   // in-degree up to which a receiver's arcs fit one half-wave pass
 
 // receiver side of a pair: half h holds receiver ks (on: the half has one;
@@ -835,15 +838,15 @@ __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
     u64x2 acc = {0, 0};
     const uint32_t nmax = max(npA, npB);
-    for (uint32_t q0 = 0; q0 < nmax; q0 += GP_ROWS_IN_FLIGHT) {
-      u64x2 r[GP_ROWS_IN_FLIGHT];
+    for (uint32_t q0 = 0; q0 < nmax; q0 += GP_PAIR_RIF) {
+      u64x2 r[GP_PAIR_RIF];
 #pragma unroll
-      for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) {
+      for (int q = 0; q < GP_PAIR_RIF; ++q) {
         r[q] = u64x2{0, 0};
         if (q0 + q < np) r[q] = load_piece<W>(a.rows, L.pre[ks][q0 + q], lw);
       }
 #pragma unroll
-      for (int q = 0; q < GP_ROWS_IN_FLIGHT; ++q) acc |= r[q];
+      for (int q = 0; q < GP_PAIR_RIF; ++q) acc |= r[q];
     }
     st.add(S_GATHERED, (u64)(npA + npB));
     st.add(S_ROW_BYTES, (u64)(npA + npB) * (u64)(8 * W));
@@ -2551,6 +2554,9 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 #ifndef GP_PARK
 #define GP_PARK 1
 #endif
+#ifndef GP_EE_DIV
+#define GP_EE_DIV 16.0
+#endif
 static int launch_expand(Ctx* c) {
   if (alive_on(c))   // F_{r+1} is built by this round's receivers
     GP_HIP(hipMemsetAsync(c->d_alive + (size_t)(c->cur ^ 1) * c->words, 0, (size_t)c->words * 8, c->stream));
@@ -2564,7 +2570,7 @@ static int launch_expand(Ctx* c) {
   // out of reach -- a message cut off by crashes -- so the done-skip alone
   // leaves nearly every receiver scanning whole rows)
   c->early_exit_now = c->cfg.early_exit != 0 &&
-                      ((double)c->prev_new_bits * 16.0 >= (double)c->n * (double)c->m ||
+                      ((double)c->prev_new_bits * GP_EE_DIV >= (double)c->n * (double)c->m ||
                        (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m);
   const u64 inj = (size_t)r < c->inj_arcs.size() ? (u64)c->inj_arcs[(size_t)r] : 0ull;
   const double est = (double)((r == 0 ? 0ull : c->prev_next_arcs) + inj);
