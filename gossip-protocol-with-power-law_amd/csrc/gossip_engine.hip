@@ -739,8 +739,10 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
 #ifndef GP_SHORT_PAIRS
 #define GP_SHORT_PAIRS 0
 #endif
+// rows in flight per half-wave in pre_pairs: 2 (70 VGPRs, 7 waves per SIMD)
+// against 4 (78, 6 waves): C4 round 1 3.97 -> 3.78 ms same-box
 #ifndef GP_PAIR_RIF
-#define GP_PAIR_RIF GP_ROWS_IN_FLIGHT
+#define GP_PAIR_RIF 2
 #endif
 constexpr int SHORT_DEG = 32;   // in-degree up to which a receiver's arcs fit one half-wave pass
 
