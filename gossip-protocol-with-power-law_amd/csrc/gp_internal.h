@@ -25,7 +25,7 @@ enum StatSlot {
   S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_ROW_BYTES,
   S_XROWS, S_XBYTES,   // boundary entries / bytes sent (vertex partition, written by the pack step)
   NST,
-  S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR
+  S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR, S_DET_BIG
 };
 
 struct HubItem {       // one wave's share of a hub's in-list
@@ -131,6 +131,11 @@ struct Ctx {
   uint8_t* d_miss = nullptr;        // [n_alloc]
   int32_t* d_deg_live = nullptr;    // [n_alloc]
   int32_t* d_cand = nullptr;        // [n] detection candidates of a round
+  int32_t* d_det_big = nullptr;     // deferred (big) detection candidates and their counters (k_det_big_*)
+  int64_t* d_det_pre = nullptr;
+  uint32_t* d_det_live = nullptr;
+  uint32_t* d_det_cur = nullptr;
+  u64* d_det_base = nullptr;
   // [n_alloc/64] frontier_r activity bitmap (fpop != 0): 2 MB at 2^24
   u64* d_abits = nullptr;
   u64* d_sbits = nullptr;   // summary level of d_abits (GP_SUMMARY_PROBE builds)

@@ -170,6 +170,28 @@ def test_unfiltered_pull_parks_crashed_rows(pkg, oracle, n, m, p_fail, flat_max_
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
+def test_detection_of_crashed_hubs(pkg, oracle, mode):
+    """Crashed vertices with more than 2048 heartbeat links are detected by the
+    grid-wide k_det_big_* kernels, the rest inside k_detect's waves: the top
+    hubs crash explicitly (and at random), reports and removals match."""
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
+    rp, col = oracle.chung_lu(60_000, 12, 2.1, 17)
+    g = pkg.CSR(60_000, rp, col, False)
+    deg = np.diff(rp)
+    hubs = np.argsort(-deg)[:6]
+    assert deg[hubs[3]] > 2048, deg[hubs]
+    origin = pkg.overlay.random_origins(g.n, 256, seed=17)
+    inject = (np.arange(256) % 3).astype(np.int32)
+    crashes = [(int(h), 1 + i % 3) for i, h in enumerate(hubs)]
+    r = _compare(pkg, oracle, g, origin, inject, crashes=crashes, churn=True, p_fail=0.02, churn_seed=23,
+                 push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words,
+                 arc_mask_permille=arc_mask)
+    assert sum(s["removals"] for s in r["stats"]) >= 6
+    assert sum(s["reports"] for s in r["stats"]) > 6 * 2048
+    r["eng"].close()
+
+
+@pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 def test_explicit_crashes_directed(pkg, oracle, mode):
     push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.first3_overlay(10)
