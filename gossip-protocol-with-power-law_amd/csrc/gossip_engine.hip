@@ -1825,16 +1825,19 @@ template <int W>
 __global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64* __restrict__ abits, uint8_t* __restrict__ ws,
                                                       u64* __restrict__ rows, int32_t rslot, int64_t n_alloc) {
   const int lane = threadIdx.x & 63;
-  const int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (w * 64 >= n_alloc) return;
-  const int64_t v0 = w * 64 + lane;
-  const bool stale = v0 < n_alloc && !((abits[w] >> lane) & 1ull) && !((ws[v0] >> rslot) & 1u);
-  u64 todo = __ballot(stale);
-  if (stale) ws[v0] |= (uint8_t)(1u << rslot);
-  while (todo) {
-    const int b = __ffsll((long long)todo) - 1;
-    todo &= todo - 1;
-    if (lane < W) rows[(size_t)(w * 64 + b) * W + lane] = 0ull;
+  // grid-stride: one wave per 64 vertices as its own launch unit was wave-
+  // dispatch-bound (0.39 ms at 2^26 for ~130 MB of bytes)
+  for (int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6); w * 64 < n_alloc;
+       w += (int64_t)gridDim.x * WAVES) {
+    const int64_t v0 = w * 64 + lane;
+    const bool stale = v0 < n_alloc && !((abits[w] >> lane) & 1ull) && !((ws[v0] >> rslot) & 1u);
+    u64 todo = __ballot(stale);
+    if (stale) ws[v0] |= (uint8_t)(1u << rslot);
+    while (todo) {
+      const int b = __ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      if (lane < W) rows[(size_t)(w * 64 + b) * W + lane] = 0ull;
+    }
   }
 }
 
@@ -1847,23 +1850,24 @@ __global__ __launch_bounds__(BLOCK) void k_park(const uint8_t* __restrict__ stat
                                                 u64* __restrict__ s0, u64* __restrict__ s1, u64* __restrict__ s2,
                                                 int64_t n_alloc) {
   const int lane = threadIdx.x & 63;
-  const int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (w * 64 >= n_alloc) return;
-  const int64_t v0 = w * 64 + lane;
-  uint32_t p = SLOT_NONE;
-  if (v0 < n_alloc && (state[v0] & ST_DOWN)) p = sp[v0];
-  const bool move = p < 2u;
-  u64 todo = __ballot(move);
-  if (move) sp[v0] = SLOT_PARKED;
-  while (todo) {
-    const int b = __ffsll((long long)todo) - 1;
-    todo &= todo - 1;
-    const uint32_t q = (uint32_t)__shfl((int)p, b);
-    if (lane < W) {
-      const size_t i = (size_t)(w * 64 + b) * W + lane;
-      s2[i] = (q ? s1 : s0)[i];
-      s0[i] = 0ull;
-      s1[i] = 0ull;
+  for (int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6); w * 64 < n_alloc;
+       w += (int64_t)gridDim.x * WAVES) {
+    const int64_t v0 = w * 64 + lane;
+    uint32_t p = SLOT_NONE;
+    if (v0 < n_alloc && (state[v0] & ST_DOWN)) p = sp[v0];
+    const bool move = p < 2u;
+    u64 todo = __ballot(move);
+    if (move) sp[v0] = SLOT_PARKED;
+    while (todo) {
+      const int b = __ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const uint32_t q = (uint32_t)__shfl((int)p, b);
+      if (lane < W) {
+        const size_t i = (size_t)(w * 64 + b) * W + lane;
+        s2[i] = (q ? s1 : s0)[i];
+        s0[i] = 0ull;
+        s1[i] = 0ull;
+      }
     }
   }
 }
@@ -1979,12 +1983,12 @@ __global__ void k_lost_clear(const int32_t* __restrict__ origin, const u64* __re
 }
 __global__ void k_done_fix(const int32_t* __restrict__ midx, const uint32_t* __restrict__ lostcnt,
                            uint32_t* __restrict__ done_at, int64_t n) {
-  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= n) return;
-  const int32_t k = midx[v];
-  if (k >= 0) {
-    const uint32_t l = lostcnt[k];
-    if (l) done_at[v] -= l;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = midx[v];
+    if (k >= 0) {
+      const uint32_t l = lostcnt[k];
+      if (l) done_at[v] -= l;
+    }
   }
 }
 
@@ -2724,10 +2728,12 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   }
   const int64_t per_block = (int64_t)WAVES * 64;
   if (a.unfiltered && c->liveness_active)
-    hipLaunchKernelGGL(k_park<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
+    hipLaunchKernelGGL(k_park<W>, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8)),
+                       dim3(BLOCK), 0, c->stream,
                        c->d_state, c->d_sp, c->d_slot[0], c->d_slot[1], c->d_slot[2], c->n_alloc);
   if (a.unfiltered)
-    hipLaunchKernelGGL(k_fixup_rows<W>, dim3(grid_for((c->n_alloc + 63) / 64, WAVES)), dim3(BLOCK), 0, c->stream,
+    hipLaunchKernelGGL(k_fixup_rows<W>, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8)),
+                       dim3(BLOCK), 0, c->stream,
                        c->d_abits, c->d_ws, c->d_slot[c->cur], c->cur, c->n_alloc);
   // W = 32 rows take the per-receiver kernel, except in dense near-done rounds
   // (most messages held, last round's new bits >= m/4 per vertex): there the
@@ -3672,7 +3678,8 @@ static int round_launch(Ctx* c) {
       hipLaunchKernelGGL(k_lost_clear, dim3(grid_for(ia.groups * c->words, 256)), dim3(256), 0, s,
                          c->d_inj_origin, c->d_inj_bits, c->d_inj_cnt, c->d_state, c->d_midx, c->d_cmask,
                          c->d_lostcnt, ia.off, ia.groups, c->words);
-      hipLaunchKernelGGL(k_done_fix, dim3(grid_for(c->n_alloc, 256)), dim3(256), 0, s, c->d_midx, c->d_lostcnt,
+      hipLaunchKernelGGL(k_done_fix, dim3(std::min(grid_for(c->n_alloc, 256), c->cu_count * 8)), dim3(256), 0, s,
+                         c->d_midx, c->d_lostcnt,
                          c->d_done_at, c->n_alloc);
       GP_HIP(hipGetLastError());
       c->done_dirty = true;
