@@ -422,6 +422,23 @@ __device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
 #ifndef GP_WORD_SKIP
 #define GP_WORD_SKIP 1
 #endif
+// Row bytes are counted per 128-B line a row load touches: HBM delivers whole
+// lines, so a lane that skips its 16 B while others of its line load theirs
+// saves no traffic (measured: skipping whole lines only, GP_LINE_SKIP in round
+// 2's notes, fetched exactly the same bytes and ran 1 ms slower).  Rows of
+// W >= 16 span whole lines (8 lanes x 16 B each); narrower rows count pieces.
+// ballot b of a row-load instruction -> 16-B pieces of the lines it touches
+template <int W>
+__device__ __forceinline__ u64 line_pieces(u64 b) {
+  if constexpr (Geo<W>::LPR >= 8) {
+    u64 t = b | (b >> 4);
+    t |= t >> 2;
+    t |= t >> 1;
+    return 8ull * (u64)__popcll(t & 0x0101010101010101ull);
+  } else {
+    return (u64)__popcll(b);
+  }
+}
 template <int W, int RIF>
 __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
                                               u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
@@ -444,9 +461,9 @@ __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t
 #pragma unroll
     for (int q = 0; q < RIF; ++q) acc |= r[q];
     st.add(S_GATHERED, (u64)min(RIF * RPI, cnt - k0));
-    u64 pieces = 0;   // 8 * WPL-byte pieces actually loaded (word skip)
+    u64 pieces = 0;   // 8 * WPL-byte pieces of the lines the loads touched (word skip)
 #pragma unroll
-    for (int q = 0; q < RIF; ++q) pieces += (u64)__popcll(__ballot(k0 + g + q * RPI < cnt && live));
+    for (int q = 0; q < RIF; ++q) pieces += line_pieces<W>(__ballot(k0 + g + q * RPI < cnt && live));
     st.add(S_ROW_BYTES, pieces * (u64)(8 * Geo<W>::WPL));
     if (ee) {
       u64x2 t = acc;
@@ -925,7 +942,7 @@ __device__ __forceinline__ void short_pairs_n(const ExpandArgs& a, LDS& L, u64 m
       for (int q = 0; q < RIF; ++q) acc |= r[q];
       uint32_t pieces = 0;
 #pragma unroll
-      for (int q = 0; q < RIF; ++q) pieces += (uint32_t)__popcll(__ballot(k0 + q < cnt && live));
+      for (int q = 0; q < RIF; ++q) pieces += (uint32_t)line_pieces<W>(__ballot(k0 + q < cnt && live));
       st.add(S_ROW_BYTES, (u64)pieces * (u64)(8 * Geo<W>::WPL));
       st.add(S_GATHERED, (u64)(min(RIF, max(cntA - k0, 0)) + min(RIF, max(cntB - k0, 0))));
       if (ee) {
