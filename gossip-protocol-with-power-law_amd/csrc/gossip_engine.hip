@@ -1371,6 +1371,9 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       st.add(S_VISITED, (u64)__popcll(needm));
     }
     const bool need = (needm >> lane) & 1ull;
+    // (a wave with no receiver to scan is done: late rounds leave most waves
+    // with none, and the passes and the receiver side cost latency even empty)
+    if (needm != 0ull) {
     if (lane < NR) {
 #pragma unroll
       for (int w = 0; w < W; ++w) F.acc[lane][w] = 0ull;
@@ -1502,6 +1505,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
     st.add(S_NEXT_ARCS, wave_sum_u64(narcs));
     st.add(S_SEEN_READ, wave_sum_u64(nseen));
     alive_flush<W>(a, F.alive, lane);
+    }   // needm
   }
   flush_stats(st, a.partial);
 }
