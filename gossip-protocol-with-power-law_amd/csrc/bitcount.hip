@@ -187,6 +187,100 @@ __global__ __launch_bounds__(BC_BLOCK) void k_bitcount(BitcountArgs a) {
   }
 }
 
+// Unweighted count at W = 64 (coverage of a churn run: every row, in vertex
+// order).  Lean enough for 8 waves per SIMD: a wave walks 16 consecutive
+// vertices per step, their 16 slot bytes are two 8-B loads made wave-uniform
+// (so each row's slot pointer is a scalar select) and issued one step ahead,
+// and the 16 rows (8 KB per wave) go in flight together.  k_bitcount kept
+// 4 KB in flight at 4 waves per SIMD and read C5's 32 GiB at 2.7 TB/s.
+__device__ __forceinline__ u64 sp_word(const uint8_t* __restrict__ sp, int64_t v, int64_t count) {
+  if (v + 8 <= count) return *reinterpret_cast<const u64*>(sp + v);
+  u64 w = ~0ull;   // past the range: empty rows
+  for (int k = 0; k < 8; ++k)
+    if (v + k < count) w = (w & ~(0xFFull << (8 * k))) | ((u64)sp[v + k] << (8 * k));
+  return w;
+}
+__global__ __launch_bounds__(BC_BLOCK) void k_bitcount_lin(BitcountArgs a) {
+  constexpr int W = 64, M = W * 64;
+  __shared__ uint32_t lc[M];
+  for (int t = threadIdx.x; t < M; t += BC_BLOCK) lc[t] = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * BC_WAVES;
+  const int64_t wid = (int64_t)blockIdx.x * BC_WAVES + wib;
+  const int64_t groups = (a.count + 15) / 16;
+  const int64_t per = (groups + nw - 1) / nw;
+  const int64_t g0 = std::min(groups, wid * per), g1 = std::min(groups, g0 + per);
+  u64 o1 = 0, o2 = 0, o4 = 0, e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) e[j] = 0;
+  int held = 0;
+  auto flush = [&]() {
+#pragma unroll 4
+    for (int b = 0; b < 64; ++b) {
+      uint32_t hi = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hi |= (uint32_t)((e[j] >> b) & 1ull) << j;
+      const uint32_t cnt = (uint32_t)((o1 >> b) & 1ull) + 2u * (uint32_t)((o2 >> b) & 1ull) +
+                           4u * (uint32_t)((o4 >> b) & 1ull) + 8u * hi;
+      if (cnt) atomicAdd(&lc[b * W + lane], cnt);
+    }
+    o1 = o2 = o4 = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = 0;
+    held = 0;
+  };
+  auto add8 = [&](const u64* x) {
+    u64 t2a, t2b, t4a, t4b, t8;
+    csa(t2a, o1, o1, x[0], x[1]);
+    csa(t2b, o1, o1, x[2], x[3]);
+    csa(t4a, o2, o2, t2a, t2b);
+    csa(t2a, o1, o1, x[4], x[5]);
+    csa(t2b, o1, o1, x[6], x[7]);
+    csa(t4b, o2, o2, t2a, t2b);
+    csa(t8, o4, o4, t4a, t4b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const u64 cj = e[j] & t8;
+      e[j] ^= t8;
+      t8 = cj;
+    }
+  };
+  u64 s0 = 0, s1 = 0;
+  if (g0 < g1) {
+    s0 = sp_word(a.sp, g0 * 16, a.count);
+    s1 = sp_word(a.sp, g0 * 16 + 8, a.count);
+  }
+  for (int64_t g = g0; g < g1; ++g) {
+    const u64 c0 = (u64)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s0) |
+                   ((u64)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(s0 >> 32)) << 32);
+    const u64 c1 = (u64)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s1) |
+                   ((u64)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(s1 >> 32)) << 32);
+    if (g + 1 < g1) {   // the next step's slot bytes, in flight with this step's rows
+      s0 = sp_word(a.sp, (g + 1) * 16, a.count);
+      s1 = sp_word(a.sp, (g + 1) * 16 + 8, a.count);
+    }
+    const int64_t v0 = g * 16;
+    u64 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t sl = (uint32_t)(((k < 8 ? c0 : c1) >> (8 * (k & 7))) & 0xFFull);
+      x[k] = sl != BC_SLOT_NONE ? a.slot[sl][(v0 + k) * W + lane] : 0ull;
+    }
+    if (held + 16 > BC_MAXCNT) flush();
+    add8(x);
+    add8(x + 8);
+    held += 16;
+  }
+  if (held > 0) flush();
+  __syncthreads();
+  uint32_t* out = a.part + (size_t)blockIdx.x * 2 * M;
+  for (int t = threadIdx.x; t < M; t += BC_BLOCK) {
+    out[t] = lc[t];
+    out[M + t] = 0u;
+  }
+}
+
 // cov / fwd += the per-block partials; blockIdx.y takes one slice of the blocks
 __global__ void k_bitcount_reduce(const uint32_t* __restrict__ part, int32_t nblocks, int32_t M,
                                   u64* __restrict__ cov, u64* __restrict__ fwd) {
@@ -300,9 +394,14 @@ static int bc_keys(Ctx* c) {
   return 0;
 }
 
+#ifndef GP_BC_LIN
+#define GP_BC_LIN 1
+#endif
 template <int W>
 static void launch_bitcount_w(Ctx* c, BitcountArgs a, bool weighted, int nblocks) {
-  if (weighted)
+  if (GP_BC_LIN && W == 64 && !weighted)   // (grid: nblocks, sized by the caller to the resident blocks)
+    hipLaunchKernelGGL(k_bitcount_lin, dim3(nblocks), dim3(BC_BLOCK), 0, c->stream, a);
+  else if (weighted)
     hipLaunchKernelGGL((k_bitcount<W, true>), dim3(nblocks), dim3(BC_BLOCK), 0, c->stream, a);
   else
     hipLaunchKernelGGL((k_bitcount<W, false>), dim3(nblocks), dim3(BC_BLOCK), 0, c->stream, a);
@@ -319,8 +418,14 @@ int bitcount_messages(Ctx* c, bool weighted, u64* cov, u64* fwd) {
   const int64_t n_all = n;
   if (weighted) n = c->bc_split;   // the tail is counted by k_bitcount_tail
   const int64_t rows_per_block = (int64_t)BC_WAVES * 512;
-  const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((n + rows_per_block - 1) / rows_per_block,
-                                                                  (int64_t)c->cu_count * 8));
+  int64_t cap = (int64_t)c->cu_count * 8;
+  if (GP_BC_LIN && W == 64 && !weighted) {   // one wave of resident blocks: equal chunks leave no tail
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bitcount_lin, BC_BLOCK, 0) == hipSuccess &&
+        per_cu > 0)
+      cap = (int64_t)c->cu_count * per_cu;
+  }
+  const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((n + rows_per_block - 1) / rows_per_block, cap));
   const size_t need = (size_t)nblocks * 2 * (size_t)M;
   if (need > c->bc_part_words) {
     GP_TRY(dalloc(&c->d_bc_part, need));
