@@ -263,6 +263,14 @@ constexpr int CML_MAXW = CML_WORDS - 1;   // nonzero words a record holds
 // when their mode is compiled out (LDS is what bounds the waves per CU)
 constexpr int PRE_IDS = 8;       // active neighbours kept per prefiltered vertex
 constexpr int PRE_MAX_DEG = 16;  // in-degree up to which the lane phase probes
+// in-degree up to which the wave probes receivers' in-lists together (SCAN_PRE
+// rounds), and how many receivers per step
+#ifndef GP_WAVE_PRE_MAX
+#define GP_WAVE_PRE_MAX 64
+#endif
+#ifndef GP_WAVE_PRE_N
+#define GP_WAVE_PRE_N 4
+#endif
 template <bool PRE, bool CML>
 struct WaveLdsT {
   static constexpr bool kPre = PRE, kCml = CML;
@@ -1094,10 +1102,66 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     wave_sync_lds();
     const bool ee = a.early_exit != 0;
     u64 m = __ballot(need);
+    if constexpr ((MODE & 3) == SCAN_PRE && GP_WAVE_PRE_MAX > PRE_MAX_DEG) {
+      // receivers with PRE_MAX_DEG < deg <= GP_WAVE_PRE_MAX: the wave probes
+      // their in-lists GP_WAVE_PRE_N at a time (one coalesced pass each, all
+      // loads in flight together) instead of one receiver's chain after the
+      // other in the serial loop; those with at most PRE_IDS active
+      // neighbours join the prefiltered receivers, those with none drop out
+      u64 mw = __ballot(need && L.np[lane] == 0xFFu && L.rp[lane + 1] - L.rp[lane] <= GP_WAVE_PRE_MAX);
+      u64 zero = 0;   // no active in-neighbour: nothing to scan (commit writes fpop_next = 0)
+      uint32_t arcs = 0;
+      while (mw) {
+        int kq[GP_WAVE_PRE_N];
+        int32_t c[GP_WAVE_PRE_N];
+#pragma unroll
+        for (int q = 0; q < GP_WAVE_PRE_N; ++q) {
+          kq[q] = -1;
+          if (mw) {
+            kq[q] = __ffsll((long long)mw) - 1;
+            mw &= mw - 1;
+          }
+          c[q] = -1;
+          if (kq[q] >= 0) {
+            const int64_t b = L.rp[kq[q]];
+            if (lane < (int)(L.rp[kq[q] + 1] - b)) c[q] = a.gcol[b + lane];
+          }
+        }
+        u64 w[GP_WAVE_PRE_N];
+#if GP_SUMMARY_PROBE
+        if (a.sbits) {
+          u64 sw[GP_WAVE_PRE_N];
+#pragma unroll
+          for (int q = 0; q < GP_WAVE_PRE_N; ++q) sw[q] = c[q] >= 0 ? a.sbits[c[q] >> 12] : 0ull;
+#pragma unroll
+          for (int q = 0; q < GP_WAVE_PRE_N; ++q)
+            w[q] = ((sw[q] >> ((c[q] >> 6) & 63)) & 1ull) ? a.abits[c[q] >> 6] : 0ull;
+        } else
+#endif
+#pragma unroll
+        for (int q = 0; q < GP_WAVE_PRE_N; ++q) w[q] = c[q] >= 0 ? a.abits[c[q] >> 6] : 0ull;
+#pragma unroll
+        for (int q = 0; q < GP_WAVE_PRE_N; ++q) {
+          if (kq[q] < 0) continue;
+          const bool act = c[q] >= 0 && ((w[q] >> (c[q] & 63)) & 1ull);
+          const u64 am = __ballot(act);
+          const int cnt = __popcll(am);
+          if (cnt <= PRE_IDS) {   // (more: the serial loop scans it, and counts its arcs)
+            if (act) L.pre[kq[q]][lane_rank(am)] = c[q];
+            if (lane == 0) L.np[kq[q]] = (uint8_t)cnt;
+            if (cnt == 0) zero |= 1ull << kq[q];
+            arcs += (uint32_t)(L.rp[kq[q] + 1] - L.rp[kq[q]]);
+          }
+        }
+      }
+      st.add(S_ARCS, (u64)arcs);
+      wave_sync_lds();
+      m &= ~zero;
+    }
     if constexpr ((MODE & SCAN_CML) != 0) L.racc[lane] = 0ull;   // record rounds: first receiver's accumulator
     if constexpr (GP_PRE_PAIRS && W == 64 && (MODE & 3) == SCAN_PRE) {
       if (!ee) {   // prefiltered receivers two at a time, the rest below
-        const u64 mp = __ballot(need && L.np[lane] != 0xFFu);
+        const u64 mp = m & __ballot(need && L.np[lane] != 0xFFu);
         pre_pairs<W>(a, L, mp, base, slot_of, st);
         m &= ~mp;
       }
