@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--compact-rows", type=int, default=0,
                     help="1: sparse 64-word rounds gather compact Message-Lists (DESIGN.md §3.2)")
     ap.add_argument("--prefilter-pct", type=int, default=20)
+    ap.add_argument("--summary-min-n", type=int, default=1 << 25,
+                    help="sparse probe rounds of overlays with >= this many vertices read the summary level first")
     ap.add_argument("--flat-max-words", type=int, default=16,
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -207,7 +209,7 @@ def main():
                            early_exit=args.early_exit,
                            unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words,
                            arc_mask_permille=args.arc_mask_permille, compact_rows=args.compact_rows,
-                           prefilter_pct=args.prefilter_pct)
+                           prefilter_pct=args.prefilter_pct, summary_min_n=args.summary_min_n)
     churn = args.workload == "c5"
     if churn:   # Bernoulli crashes of live vertices, stream seeded by the run seed
         eng.configure(churn=1, p_fail=args.p_fail, churn_seed=args.seed, miss_threshold=3)

@@ -597,19 +597,25 @@ def test_wide_rows_no_churn(pkg, oracle, mode):
 
 
 @pytest.mark.parametrize("prefilter", [0, 20])
-def test_compact_message_lists(pkg, oracle, prefilter):
+@pytest.mark.parametrize("churn", [False, True])
+def test_compact_message_lists(pkg, oracle, prefilter, churn):
     """W = 64, every message injected at round 0 on a sparse overlay: the early
-    rounds gather senders from compact Message-Lists (scan bit 4), with and
-    without the lane-parallel prefilter; results are those of the oracle and of
-    a run with compact rows off."""
+    rounds gather senders from compact Message-Lists (scan bit 4; receivers of
+    up to GP_QUAD_DEG in-arcs four at a time in rec_quads, the rest one at a
+    time), with and without the lane-parallel prefilter, with churn (exact
+    frontier rows, alive sets); results are those of the oracle (first-receipt
+    matrix included) and of a run with compact rows off."""
     rp, col = oracle.chung_lu(200_000, 8, 2.5, 31)
     g = pkg.CSR(200_000, rp, col, False)
     origin = pkg.overlay.random_origins(g.n, 4096, seed=31)
-    r = _compare(pkg, oracle, g, origin, first=False, push_ratio=0.0, prefilter_pct=prefilter, arc_mask_permille=0,
-                 compact_rows=1)
+    kw = dict(churn=True, p_fail=0.01, churn_seed=3) if churn else {}
+    r = _compare(pkg, oracle, g, origin, first=True, push_ratio=0.0, prefilter_pct=prefilter, arc_mask_permille=0,
+                 compact_rows=1, **kw)
     assert any(s["scan"] & 4 for s in r["stats"])
     assert any((s["scan"] & 3) == (3 if prefilter else 0) and s["scan"] & 4 for s in r["stats"])
     r["eng"].close()
+    if churn:
+        return
     with pkg.GossipEngine(0, track_digest=1, push_ratio=0.0, prefilter_pct=prefilter, compact_rows=0,
                           arc_mask_permille=0, unfiltered_pct=90, flat_max_words=16, hub_threshold=4096) as eng:
         eng.load_graph(g)
