@@ -63,7 +63,8 @@ def parse():
                     help="cpu_baseline: overlay size of the oracle's bounded sample (all messages, W = 64)")
     ap.add_argument("--parallel", choices=("messages", "vertex"), default="messages",
                     help="N > 1: message shards (no data-path collective, default) or the vertex "
-                         "partition with an RCCL all-gather of the next rows every round")
+                         "partition with a sparse boundary exchange every round (ncclSend/Recv of "
+                         "the boundary vertices' new words)")
     ap.add_argument("--profile-steps", action="store_true",
                     help="print per-round stats of the last step to stderr")
     a = ap.parse_args()
@@ -257,8 +258,9 @@ def main():
         rounds = int(dist.allmax(pg, rounds))
     exp_ms = sum(s["expand_ms"] for r in runs for s in r)
     exch_ms = sum(s["exchange_ms"] for r in runs for s in r)
-    # roofline of the dominant kernel, k_expand: its pull rounds only, its own
-    # HIP-event time (kernel_ms); alg bytes include the small hub passes' share
+    # roofline of the dominant kernel set, the pull: k_expand (or k_expand_flat)
+    # plus the hub passes that finish its hub receivers -- HIP events bracket
+    # all three (kernel_ms), and the algorithmic bytes count all three
     pulls = [s for r in runs for s in r if s["mode"] == 0 and s["kernel_ms"] > 0]
     nbytes = sum(round_bytes(s, eng.words, n) for s in pulls)
     kern_ms = sum(s["kernel_ms"] for s in pulls)
@@ -299,7 +301,8 @@ def main():
                        "words_per_row": eng.words, "rounds_per_step": rounds / args.steps,
                        "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,
                        "parallelism": (f"message-shard x{world} (no data-path collective)" if shards else
-                                       f"vertex-partition x{world}" + (" (RCCL all-gather)" if world > 1 else "")),
+                                       f"vertex-partition x{world}" + (" (sparse boundary exchange, ncclSend/Recv)"
+                                                                      if world > 1 else "")),
                        "setup_s": round(setup_s, 2), "build_s": round(build_s, 2),
                        "degree_check": {"gamma_hat": round(deg["gamma_hat"], 4), "kmin": deg["kmin"],
                                         "gamma": args.gamma, "ok": bool(deg["ok"])}},
@@ -307,7 +310,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": (f"k_expand<{eng.words}>" if eng.words > 32 else
                                     f"k_expand<{eng.words}> / k_expand_flat<{eng.words}>")
-                                   + ", HIP events on the engine stream",
+                                   + " + k_hub_partial + k_hub_final per pull launch, HIP events on the "
+                                     "engine stream",
                          "launches": len(pulls),
                          "avg_launch_ms": kern_ms / max(len(pulls), 1),
                          "alg_bytes_per_launch": nbytes / max(len(pulls), 1),

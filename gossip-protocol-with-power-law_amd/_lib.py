@@ -86,6 +86,8 @@ class Config(ctypes.Structure):
         ("msg_word_base", ctypes.c_int32),
         ("flat_max_words", ctypes.c_int32),
         ("summary_min_n", ctypes.c_int64),
+        ("partition_by_arcs", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
     ]
 
 
@@ -124,7 +126,7 @@ SIGNATURES = {
     "gp_checkpoint_load": (ctypes.c_int, [_P, _P, _I64]),
 }
 
-ABI_VERSION = 12   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 13   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

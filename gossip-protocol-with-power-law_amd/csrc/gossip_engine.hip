@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "gp_internal.h"
+#include "xplan.h"
 
 namespace gp {
 
@@ -2892,7 +2893,6 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
         hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
     }
   }
-  (void)hipEventRecord(c->ev[5], c->stream);
   if (c->n_hub_items > 0) {
     ExpandArgs h = a;
     h.n_items = c->n_hub_items;
@@ -2904,6 +2904,9 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     h.n_items = c->n_hubs;
     hipLaunchKernelGGL(k_hub_final<W>, dim3(grid_for(h.n_items, WAVES)), dim3(BLOCK), 0, c->stream, h);
   }
+  // kernel_ms brackets the pull kernel and the hub passes: the round's
+  // counters (row bytes, arcs scanned, rows written) include the hubs' share
+  (void)hipEventRecord(c->ev[5], c->stream);
 }
 
 #ifndef GP_PARK
@@ -3078,9 +3081,10 @@ static int set_partition(Ctx* c, int32_t rank, int32_t nranks) {
     return set_error(GP_EINVAL, "vertex partitions need an undirected overlay (ghost rows are in-neighbours)");
   c->rank = rank;
   c->nranks = nranks;
-  c->slice = (c->n + nranks - 1) / nranks;
-  c->vbegin = std::min(c->n, (int64_t)rank * c->slice);
-  c->vend = std::min(c->n, c->vbegin + c->slice);
+  c->h_bounds = partition_bounds(c->n, nranks, c->cfg.partition_by_arcs,
+                                 c->h_row_ptr.size() == (size_t)c->n + 1 ? c->h_row_ptr.data() : nullptr);
+  c->vbegin = c->h_bounds[(size_t)rank];
+  c->vend = c->h_bounds[(size_t)rank + 1];
   c->n_alloc = c->n;
   c->base_nv = c->n;
   if (nranks > 1) {   // local ids from here on: the message table must be set again
@@ -3357,6 +3361,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->msg_word_base = 0;
   cfg->flat_max_words = 16;
   cfg->summary_min_n = 1ll << 25;   // activity bitmap > 4 MB: outgrows an XCD's L2
+  cfg->partition_by_arcs = 0;       // vertex partitions: equal vertex counts (1: equal arc counts)
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -3425,6 +3430,10 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->summary_min_n < 0) return set_error(GP_EINVAL, "summary_min_n < 0");
   if (cfg->compact_rows != 0 && cfg->compact_rows != 1) return set_error(GP_EINVAL, "compact_rows must be 0 or 1");
   if (cfg->arc_mask_permille < 0) return set_error(GP_EINVAL, "arc_mask_permille < 0");
+  if (cfg->partition_by_arcs != 0 && cfg->partition_by_arcs != 1)
+    return set_error(GP_EINVAL, "partition_by_arcs must be 0 or 1");
+  if (c->local && cfg->partition_by_arcs != c->cfg.partition_by_arcs)
+    return set_error(GP_ESTATE, "a partitioned context keeps its partition: reload the overlay to change it");
   GP_HIP(hipSetDevice(c->device));
   const bool hub_changed = cfg->hub_threshold != c->cfg.hub_threshold;
   c->cfg = *cfg;

@@ -60,7 +60,7 @@ struct Ctx {
   // global id, hence grouped by owner -- then the message origins that are
   // neither ("extras", so that every rank sees every origin's liveness).
   int32_t rank = 0, nranks = 1;
-  int64_t slice = 0;                  // owned vertices per rank (ceil(n / nranks))
+  std::vector<int64_t> h_bounds;      // [nranks + 1] owned slices (xplan.h partition_bounds)
   int64_t vbegin = 0, vend = 0;       // owned vertices, GLOBAL ids
   int64_t n_alloc = 0;                // local vertex slots: nloc + nghost + nextra
   bool local = false;                 // vertex-partitioned (local ids != global ids)
@@ -96,6 +96,7 @@ struct Ctx {
   u64* d_cnt = nullptr;               // [4 * nranks] per peer: head start, heads, word start, words
   u64* d_cnt_all = nullptr;           // [nranks][4 * nranks]
   u64* h_cnt_all = nullptr;           // pinned copy
+  std::vector<int64_t> h_ghosts_all;  // [nranks][nranks] ghosts rank d holds of owner q (checked once)
   u64* d_alive_all = nullptr;         // [nranks][W]
   void* d_scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;

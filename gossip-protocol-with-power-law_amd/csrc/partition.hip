@@ -44,6 +44,7 @@
 #include <vector>
 
 #include "gp_internal.h"
+#include "xplan.h"
 
 namespace gp {
 
@@ -79,6 +80,7 @@ void free_partition(Ctx* c) {
   c->nghost = c->nextra = 0;
   c->n_bnd = c->n_bvx = 0;
   c->h_l2g.clear(); c->h_comp_g.clear(); c->h_bnd_ptr.clear(); c->h_gh_ptr.clear();
+  c->h_ghosts_all.clear();
 }
 
 template <class T>
@@ -104,7 +106,7 @@ static int upload_vertex_tables(Ctx* c) {
 
 // global CSR (device + host row_ptr) -> this rank's local CSR and boundary lists
 int localize(Ctx* c) {
-  const int64_t n = c->n, P = c->nranks, p = c->rank, S = c->slice;
+  const int64_t n = c->n, P = c->nranks, p = c->rank;
   const int64_t vb = c->vbegin, ve = c->vend, nl = ve - vb;
   if (P > MAX_PARTS) return set_error(GP_EINVAL, "at most 64 ranks per vertex partition");
   const std::vector<int64_t>& rp = c->h_row_ptr;   // global row_ptr (finish_graph)
@@ -115,7 +117,7 @@ int localize(Ctx* c) {
   GP_TRY(copy_sync(c, gcol.data(), c->d_gcol + a0, gcol.size() * 4, hipMemcpyDeviceToHost));
   c->h_comp_g.resize((size_t)n);
   GP_TRY(copy_sync(c, c->h_comp_g.data(), c->d_comp, (size_t)n * 4, hipMemcpyDeviceToHost));
-  auto owner = [&](int64_t u) { return u / S; };
+  auto owner = [&](int64_t u) { return owner_of(c->h_bounds, u); };
 
   // ghosts: non-owned in-neighbours of owned vertices, sorted
   std::vector<uint8_t> mark((size_t)n, 0);
@@ -129,7 +131,7 @@ int localize(Ctx* c) {
   c->h_gh_ptr.assign((size_t)P + 1, 0);
   for (int64_t q = 0; q <= P; ++q)
     c->h_gh_ptr[(size_t)q] =
-        std::lower_bound(ghosts.begin(), ghosts.end(), (int32_t)std::min(n, q * S)) - ghosts.begin();
+        std::lower_bound(ghosts.begin(), ghosts.end(), (int32_t)c->h_bounds[(size_t)q]) - ghosts.begin();
   std::vector<int32_t> g2l((size_t)n, -1);
   for (int64_t i = 0; i < nl; ++i) g2l[(size_t)(vb + i)] = (int32_t)i;
   for (int64_t k = 0; k < ng; ++k) g2l[(size_t)ghosts[(size_t)k]] = (int32_t)(nl + k);
@@ -197,10 +199,8 @@ int localize(Ctx* c) {
       }
     }
   }
-  // B_pq and rank q's ghosts of owner p must be the same list
-  for (int64_t q = 0; q < P; ++q)
-    if (q != p && c->h_gh_ptr[(size_t)q + 1] - c->h_gh_ptr[(size_t)q] < 0)
-      return set_error(GP_EINVAL, "ghost table inconsistent");
+  // B_pq and rank q's ghosts of owner p must be the same list: their lengths
+  // are compared across ranks before the first exchange (check_lists_*)
 
   // install: local CSR replaces the global one
   c->h_l2g.resize((size_t)nv);
@@ -484,10 +484,58 @@ static int unpack_received(Ctx* c, const std::vector<int64_t>& rk) {
 
 static bool alive_reduce_on(const Ctx* c) { return c->d_alive != nullptr && c->liveness_active; }
 
+// this rank's send-list lengths |B_pq| and ghost counts per owner q
+static void list_lengths(const Ctx* c, int64_t* bnd, int64_t* gh) {
+  for (int64_t q = 0; q < c->nranks; ++q) {
+    bnd[q] = q == c->rank ? 0 : c->h_bnd_ptr[(size_t)q + 1] - c->h_bnd_ptr[(size_t)q];
+    gh[q] = q == c->rank ? 0 : c->h_gh_ptr[(size_t)q + 1] - c->h_gh_ptr[(size_t)q];
+  }
+}
+
+// once per partition, on every rank: all-gather (|B_pq|, ghosts of q) and
+// compare them pairwise (xplan_check_lists); every rank gets the same answer
+static int check_lists_rccl(Ctx* c) {
+  if (!c->h_ghosts_all.empty()) return 0;
+  hipStream_t s = c->stream;
+  const int64_t P = c->nranks;
+  std::vector<u64> mine(2 * (size_t)P), all(2 * (size_t)(P * P));
+  std::vector<int64_t> bnd((size_t)P), gh((size_t)P);
+  list_lengths(c, bnd.data(), gh.data());
+  for (int64_t q = 0; q < P; ++q) {
+    mine[(size_t)q] = (u64)bnd[(size_t)q];
+    mine[(size_t)(P + q)] = (u64)gh[(size_t)q];
+  }
+  GP_HIP(hipMemcpyAsync(c->d_cnt, mine.data(), mine.size() * 8, hipMemcpyHostToDevice, s));
+  GP_RCCL(ncclAllGather(c->d_cnt, c->d_cnt_all, 2 * (size_t)P, ncclUint64, c->comm, s));
+  GP_HIP(hipMemcpyAsync(all.data(), c->d_cnt_all, all.size() * 8, hipMemcpyDeviceToHost, s));
+  GP_HIP(hipStreamSynchronize(s));
+  std::vector<int64_t> bnd_all((size_t)(P * P)), gh_all((size_t)(P * P));
+  for (int64_t r = 0; r < P; ++r)
+    for (int64_t q = 0; q < P; ++q) {
+      bnd_all[(size_t)(r * P + q)] = (int64_t)all[(size_t)(r * 2 * P + q)];
+      gh_all[(size_t)(r * P + q)] = (int64_t)all[(size_t)(r * 2 * P + P + q)];
+    }
+  std::string err;
+  if (!xplan_check_lists(bnd_all.data(), gh_all.data(), (int)P, &err)) return set_error(GP_EINVAL, err);
+  c->h_ghosts_all = std::move(gh_all);
+  return 0;
+}
+
+static int check_lists_group(Ctx** ctxs, int32_t P) {
+  if (!ctxs[0]->h_ghosts_all.empty()) return 0;
+  std::vector<int64_t> bnd_all((size_t)P * P), gh_all((size_t)P * P);
+  for (int32_t k = 0; k < P; ++k) list_lengths(ctxs[k], &bnd_all[(size_t)k * P], &gh_all[(size_t)k * P]);
+  std::string err;
+  if (!xplan_check_lists(bnd_all.data(), gh_all.data(), P, &err)) return set_error(GP_EINVAL, err);
+  for (int32_t k = 0; k < P; ++k) ctxs[k]->h_ghosts_all = gh_all;
+  return 0;
+}
+
 int exchange_rccl(Ctx* c) {
   hipStream_t s = c->stream;
   const int64_t P = c->nranks, p = c->rank;
   const size_t W = (size_t)c->words;
+  GP_TRY(check_lists_rccl(c));
   GP_TRY(pack_boundary(c));
   u64* alive_next = c->d_alive + (size_t)(c->cur ^ 1) * W;
   GP_RCCL(ncclGroupStart());
@@ -499,43 +547,44 @@ int exchange_rccl(Ctx* c) {
                                              (int32_t)W, alive_next);
   GP_HIP(hipMemcpyAsync(c->h_cnt_all, c->d_cnt_all, 4 * (size_t)(P * P) * sizeof(u64), hipMemcpyDeviceToHost, s));
   GP_HIP(hipStreamSynchronize(s));
-  const u64* all = c->h_cnt_all;   // [sender][4 * receiver]
-  std::vector<int64_t> rk((size_t)P + 1, 0), rw((size_t)P + 1, 0);
-  for (int64_t q = 0; q < P; ++q) {
-    const bool peer = q != p;
-    rk[(size_t)q + 1] = rk[(size_t)q] + (peer ? (int64_t)all[q * 4 * P + 4 * p + 1] : 0);
-    rw[(size_t)q + 1] = rw[(size_t)q] + (peer ? (int64_t)all[q * 4 * P + 4 * p + 3] : 0);
-  }
-  if (rk[(size_t)P] > c->nghost) return set_error(GP_EINVAL, "exchange: more entries than ghosts");
+  // every rank checks every receiver's counts: all return, or none does
+  std::string err;
+  if (!xplan_check_all(c->h_cnt_all, (int)P, c->h_ghosts_all.data(), (int)W, &err))
+    return set_error(GP_EINVAL, err);
+  XPlan plan;
+  (void)xplan_build(c->h_cnt_all, (int)P, (int)p, &c->h_ghosts_all[(size_t)(p * P)], (int)W, &plan, &err);
   GP_RCCL(ncclGroupStart());
   for (int64_t q = 0; q < P; ++q) {
     if (q == p) continue;
-    const u64* mine = all + p * 4 * P + 4 * q;   // what this rank sends to q
-    if (mine[1]) {
-      GP_RCCL(ncclSend(c->d_sbuf_h + mine[0], mine[1], ncclUint64, (int)q, c->comm, s));
-      GP_RCCL(ncclSend(c->d_sbuf_w + mine[2], mine[3], ncclUint64, (int)q, c->comm, s));
+    const XSlice& out = plan.send[(size_t)q];
+    if (out.nh) {
+      GP_RCCL(ncclSend(c->d_sbuf_h + out.h0, (size_t)out.nh, ncclUint64, (int)q, c->comm, s));
+      GP_RCCL(ncclSend(c->d_sbuf_w + out.w0, (size_t)out.nw, ncclUint64, (int)q, c->comm, s));
     }
-    const int64_t kh = rk[(size_t)q + 1] - rk[(size_t)q], kw = rw[(size_t)q + 1] - rw[(size_t)q];
-    if (kh) {
-      GP_RCCL(ncclRecv(c->d_rbuf_h + rk[(size_t)q], (size_t)kh, ncclUint64, (int)q, c->comm, s));
-      GP_RCCL(ncclRecv(c->d_rbuf_w + rw[(size_t)q], (size_t)kw, ncclUint64, (int)q, c->comm, s));
+    const XSlice& in = plan.recv[(size_t)q];
+    if (in.nh) {
+      GP_RCCL(ncclRecv(c->d_rbuf_h + in.h0, (size_t)in.nh, ncclUint64, (int)q, c->comm, s));
+      GP_RCCL(ncclRecv(c->d_rbuf_w + in.w0, (size_t)in.nw, ncclUint64, (int)q, c->comm, s));
     }
   }
   GP_RCCL(ncclGroupEnd());
-  return unpack_received(c, rk);
+  return unpack_received(c, plan.rk);
 }
 
 int exchange_group(Ctx** ctxs, int32_t P) {
+  GP_TRY(check_lists_group(ctxs, P));
   for (int32_t k = 0; k < P; ++k) {
     GP_HIP(hipSetDevice(ctxs[k]->device));
     GP_TRY(pack_boundary(ctxs[k]));
   }
-  std::vector<std::vector<u64>> cnt((size_t)P, std::vector<u64>(4 * (size_t)P));
+  // the count matrix as the RCCL path all-gathers it: [sender][4 * receiver]
+  std::vector<u64> all(4 * (size_t)P * P);
   for (int32_t k = 0; k < P; ++k) {
     Ctx* c = ctxs[k];
     GP_HIP(hipSetDevice(c->device));
     GP_HIP(hipStreamSynchronize(c->stream));
-    GP_TRY(copy_sync(c, cnt[(size_t)k].data(), c->d_cnt, 4 * (size_t)P * sizeof(u64), hipMemcpyDeviceToHost));
+    GP_TRY(copy_sync(c, all.data() + 4 * (size_t)P * k, c->d_cnt, 4 * (size_t)P * sizeof(u64),
+                     hipMemcpyDeviceToHost));
   }
   // alive sets: OR of every context's partial set
   if (alive_reduce_on(ctxs[0])) {
@@ -551,26 +600,25 @@ int exchange_group(Ctx** ctxs, int32_t P) {
       GP_TRY(copy_sync(c, c->d_alive + (size_t)(c->cur ^ 1) * W, acc.data(), W * 8, hipMemcpyHostToDevice));
     }
   }
+  std::string err;
+  const int W = ctxs[0]->words;
+  if (!xplan_check_all(all.data(), P, ctxs[0]->h_ghosts_all.data(), W, &err)) return set_error(GP_EINVAL, err);
   for (int32_t d = 0; d < P; ++d) {
     Ctx* dst = ctxs[d];
     GP_HIP(hipSetDevice(dst->device));
-    std::vector<int64_t> rk((size_t)P + 1, 0), rw((size_t)P + 1, 0);
+    XPlan plan;
+    (void)xplan_build(all.data(), P, d, &dst->h_ghosts_all[(size_t)d * P], W, &plan, &err);
     for (int32_t q = 0; q < P; ++q) {
-      const u64* src = cnt[(size_t)q].data() + 4 * d;   // what q sends to d
-      const bool peer = q != d;
-      rk[(size_t)q + 1] = rk[(size_t)q] + (peer ? (int64_t)src[1] : 0);
-      rw[(size_t)q + 1] = rw[(size_t)q] + (peer ? (int64_t)src[3] : 0);
-    }
-    if (rk[(size_t)P] > dst->nghost) return set_error(GP_EINVAL, "exchange: more entries than ghosts");
-    for (int32_t q = 0; q < P; ++q) {
-      const u64* src = cnt[(size_t)q].data() + 4 * d;
-      if (q == d || !src[1]) continue;
-      GP_HIP(hipMemcpyAsync(dst->d_rbuf_h + rk[(size_t)q], ctxs[q]->d_sbuf_h + src[0], src[1] * 8, hipMemcpyDefault,
+      if (q == d) continue;
+      const XSlice& in = plan.recv[(size_t)q];
+      if (!in.nh) continue;
+      const XSlice& out = xplan_send_of(all.data(), P, q, d);
+      GP_HIP(hipMemcpyAsync(dst->d_rbuf_h + in.h0, ctxs[q]->d_sbuf_h + out.h0, (size_t)in.nh * 8, hipMemcpyDefault,
                             dst->stream));
-      GP_HIP(hipMemcpyAsync(dst->d_rbuf_w + rw[(size_t)q], ctxs[q]->d_sbuf_w + src[2], src[3] * 8, hipMemcpyDefault,
+      GP_HIP(hipMemcpyAsync(dst->d_rbuf_w + in.w0, ctxs[q]->d_sbuf_w + out.w0, (size_t)in.nw * 8, hipMemcpyDefault,
                             dst->stream));
     }
-    GP_TRY(unpack_received(dst, rk));
+    GP_TRY(unpack_received(dst, plan.rk));
   }
   return 0;
 }

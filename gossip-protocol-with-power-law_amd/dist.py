@@ -7,8 +7,10 @@ Two ways to spread one gossip run over N GPUs:
   for the word-aligned message block message_shard(m, N, p).  No data-path
   collective: the shards' per-round counters add up, their digests XOR, their
   first / coverage / forwards columns concatenate.
-* vertex partition: rank p owns the contiguous vertex slice [p*S, min((p+1)*S, n))
-  with S = ceil(n / nranks); every round each rank ships the new frontier words
+* vertex partition: rank p owns a contiguous vertex slice, by default
+  [p*S, min((p+1)*S, n)) with S = ceil(n / nranks), or with
+  partition_by_arcs=1 the slice holding in-arcs [p*A/N, (p+1)*A/N) (SURVEY.md
+  §8e; partition_bounds below mirrors csrc/xplan.h); every round each rank ships the new frontier words
   of its boundary vertices to the ranks holding them as ghosts (ncclSend /
   ncclRecv inside libgossip_hip.so, csrc/partition.hip).
 
@@ -47,9 +49,23 @@ def message_shard(m, nranks, rank):
     return min(m, 64 * w0), min(m, 64 * w1)
 
 
-def partition_bounds(n, nranks):
+def partition_bounds(n, nranks, row_ptr=None):
+    """Owned slices [(begin, end)] of a vertex partition, as the engine cuts
+    them (csrc/xplan.h partition_bounds): equal vertex counts, or, given the
+    global in-CSR row_ptr (partition_by_arcs=1), equal in-arc counts --
+    rank p starts at the first vertex whose arcs start at or after
+    ceil(p * nnz / nranks)."""
+    b = [0] * (nranks + 1)
+    b[nranks] = n
+    nnz = int(row_ptr[n]) if row_ptr is not None else 0
     s = (n + nranks - 1) // nranks
-    return [(min(n, p * s), min(n, (p + 1) * s)) for p in range(nranks)]
+    for p in range(1, nranks):
+        if row_ptr is not None and nnz > 0:
+            b[p] = int(np.searchsorted(row_ptr, (p * nnz + nranks - 1) // nranks, side="left"))
+        else:
+            b[p] = min(n, p * s)
+        b[p] = max(b[p], b[p - 1])
+    return [(b[p], b[p + 1]) for p in range(nranks)]
 
 
 # ---------------------------------------------------------------------------

@@ -7,6 +7,7 @@ removal (Seed.py:358-406).  One `round()` = liveness + injection + pull
 expansion (+ RCCL exchange on multi-GPU), all on the device.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -232,15 +233,27 @@ class GossipEngine:
     def save_checkpoint(self, path):
         """Write the checkpoint() blob to `path` as a .npy file, straight into a
         memory map of the file: host memory stays bounded by the page cache
-        even for the 32 GiB of Message-List rows of a 2^26 x 4096 run."""
+        even for the 32 GiB of Message-List rows of a 2^26 x 4096 run.  The
+        blob goes to `path`.tmp first and replaces `path` only once it is
+        complete, so a failed save leaves the previous checkpoint intact."""
         nb = ctypes.c_int64()
         check(self._lib.gp_checkpoint_size(self._ctx, ctypes.byref(nb)))
-        out = np.lib.format.open_memmap(path, mode="w+", dtype=np.uint8, shape=(nb.value,))
+        path = os.fspath(path)
+        tmp = path + ".tmp"
+        out = np.lib.format.open_memmap(tmp, mode="w+", dtype=np.uint8, shape=(nb.value,))
+        ok = False
         try:
             check(self._lib.gp_checkpoint_save(self._ctx, _ptr(out), out.nbytes))
             out.flush()
+            ok = True
         finally:
             del out
+            if not ok:
+                try:
+                    os.unlink(tmp)
+                except OSError:
+                    pass
+        os.replace(tmp, path)
 
     def load_checkpoint(self, path):
         """Restore a save_checkpoint() file (memory-mapped, read-only).  The
@@ -298,9 +311,12 @@ class GossipEngine:
 
     def reports(self, cap=1 << 20):
         """Reports of the last round as int32 [k, 3] (dead, reporter, round),
-        unordered, plus the exact total (k < total if the buffer overflowed)."""
+        unordered, plus the exact total (k < total if the buffer overflowed).
+        gp_reports copies at most min(total, cap, report_capacity) rows: only
+        those are returned."""
         buf = np.empty((cap, 3), dtype=np.int32)
         n = ctypes.c_int64()
         check(self._lib.gp_reports(self._ctx, ctypes.cast(buf.ctypes.data, ctypes.POINTER(_lib.Report)),
                                    int(cap), ctypes.byref(n)))
-        return buf[:min(n.value, cap)].copy(), n.value
+        k = min(n.value, cap, max(int(self.cfg.report_capacity), 1))
+        return buf[:k].copy(), n.value

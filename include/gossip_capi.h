@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 12
+#define GP_ABI_VERSION 13
 
 typedef struct gp_ctx gp_ctx;
 
@@ -89,7 +89,7 @@ typedef struct gp_round_stats {
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
-  double kernel_ms;         /* device time of the main pull kernel k_expand alone    */
+  double kernel_ms;         /* device time of the pull kernel + its hub passes       */
   uint64_t xchg_rows;       /* vertex partition: boundary entries sent (all peers)   */
   uint64_t xchg_bytes;      /* vertex partition: bytes sent (entry heads + words)    */
 } gp_round_stats;
@@ -134,6 +134,10 @@ typedef struct gp_config {
                                   vertices, with at most n/256 senders, probe a summary
                                   level (1 bit per 64 vertices) before the activity
                                   bitmap (0 = never)                    */
+  int32_t partition_by_arcs;   /* vertex partitions (gp_set_partition): 0 = slices of equal
+                                  vertex count, 1 = slices of equal in-arc count
+                                  (set before the partition is made)     */
+  int32_t reserved0;           /* zero                                                   */
 } gp_config;
 
 /* what for gp_read */

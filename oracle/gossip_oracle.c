@@ -18,7 +18,10 @@
  *    per-peer Message-List harness oracle/harness.py (sha256 dedup).
  *
  * Written as straightforward scalar loops (no bitmap tricks beyond the u64 packing
- * that defines the Message-List), OpenMP over vertices for the timed baseline.
+ * that defines the Message-List), OpenMP over vertices: the expansion, the
+ * per-message forwards (fused into the expansion pass) and the coverage count
+ * all run on every thread, so the full 2^24 x 4096 run (BASELINE config 4)
+ * finishes in about a minute on 16 host cores.
  */
 #include <math.h>
 #include <stdint.h>
@@ -190,6 +193,16 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
   int32_t* deg_live = (int32_t*)malloc((size_t)n * 4);
   int32_t* cand = (int32_t*)malloc((size_t)n * 4);
   uint64_t* fwd = (uint64_t*)calloc((size_t)W * 64, 8);
+  /* fz[v]: frontier row of v non-zero (senders with an empty frontier are skipped:
+     OR-ing a zero row changes nothing) */
+  uint8_t* fz = (uint8_t*)calloc((size_t)n, 1);
+  uint8_t* fz_next = (uint8_t*)calloc((size_t)n, 1);
+  int nth = 1;
+#ifdef _OPENMP
+  nth = omp_get_max_threads();
+#endif
+  /* per-thread per-message accumulators (forwards, coverage), summed after each pass */
+  uint64_t* acc_t = (uint64_t*)calloc((size_t)nth * W * 64, 8);
   if (first_out) memset(first_out, 0xFF, (size_t)n * m);
   const int64_t* drp = directed ? out_row_ptr : row_ptr;
   for (int64_t v = 0; v < n; ++v) deg_live[v] = (int32_t)(drp[v + 1] - drp[v]);
@@ -217,6 +230,7 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
           if (crash) {
             state[v] |= ST_CRASHED;
             memset(front + (size_t)v * W, 0, (size_t)W * 8);
+            fz[v] = 0;
             st.crashed++;
           }
         }
@@ -261,6 +275,7 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
         continue;
       }
       front[(size_t)o * W + (k >> 6)] |= 1ull << (k & 63);
+      fz[o] = 1;
       seen[(size_t)o * W + (k >> 6)] |= 1ull << (k & 63);
       if (first_out) first_out[(size_t)o * m + k] = (uint8_t)r;
       st.injected++;
@@ -277,62 +292,79 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
         if (inject_round[j] == r && origin[j] == o && (j >> 6) == (k >> 6)) bits |= 1ull << (j & 63);
       digest[o] ^= or_term((uint32_t)r, (uint32_t)(k >> 6) | OR_INJ, bits);
     }
-    /* per-message forwards of round r: every holder sends to its live links */
-    if (forwards_out) {
-      for (int64_t v = 0; v < n; ++v) {
-        const uint64_t* f = front + (size_t)v * W;
-        for (int w = 0; w < W; ++w) {
-          uint64_t x = f[w];
-          while (x) {
-            int b = __builtin_ctzll(x);
-            fwd[w * 64 + b] += (uint64_t)(deg_live[v] > 0 ? deg_live[v] : 0);
-            x &= x - 1;
-          }
-        }
-      }
-    }
-    /* E_r: pull expansion with forward-once dedup against the Message-List `seen` */
+    /* E_r: pull expansion with forward-once dedup against the Message-List `seen`;
+       the same pass adds round r's per-message forwards: every holder of message k
+       in its frontier sends it to its live links (thread-local, summed below) */
     int64_t s_new = 0, s_recv = 0, s_sends = 0, s_active = 0;
-#pragma omp parallel for schedule(dynamic, 512) reduction(+ : s_new, s_recv, s_sends, s_active)
-    for (int64_t v = 0; v < n; ++v) {
-      const uint64_t* fv = front + (size_t)v * W;
-      int64_t pc = 0;
-      for (int w = 0; w < W; ++w) pc += popc64(fv[w]);
-      if (pc) {
-        s_sends += pc * (int64_t)(deg_live[v] > 0 ? deg_live[v] : 0);
-        s_active++;
-      }
-      uint64_t* nx = next + (size_t)v * W;
-      if (state[v] & ST_DOWN) {
-        memset(nx, 0, (size_t)W * 8);
-        continue;
-      }
-      int64_t newc = 0;
-      uint64_t acc[64];
-      for (int w = 0; w < W; ++w) acc[w] = 0;
-      for (int64_t j = row_ptr[v]; j < row_ptr[v + 1]; ++j) {
-        const uint64_t* fu = front + (size_t)col[j] * W;
-        for (int w = 0; w < W; ++w) acc[w] |= fu[w];
-      }
-      for (int w = 0; w < W; ++w) {
-        uint64_t nw = acc[w] & ~seen[(size_t)v * W + w];
-        nx[w] = nw;
-        if (!nw) continue;
-        seen[(size_t)v * W + w] |= nw;
-        newc += popc64(nw);
-        digest[v] ^= or_term((uint32_t)(r + 1), (uint32_t)w, nw);
-        if (first_out) {
-          uint64_t x = nw;
-          while (x) {
-            int b = __builtin_ctzll(x);
-            first_out[(size_t)v * m + w * 64 + b] = (uint8_t)(r + 1);
-            x &= x - 1;
+    const int want_fwd = forwards_out != NULL;
+#pragma omp parallel reduction(+ : s_new, s_recv, s_sends, s_active)
+    {
+      int tid = 0;
+#ifdef _OPENMP
+      tid = omp_get_thread_num();
+#endif
+      uint64_t* my_fwd = acc_t + (size_t)tid * W * 64;
+#pragma omp for schedule(dynamic, 512)
+      for (int64_t v = 0; v < n; ++v) {
+        const uint64_t* fv = front + (size_t)v * W;
+        const uint64_t dl = (uint64_t)(deg_live[v] > 0 ? deg_live[v] : 0);
+        int64_t pc = 0;
+        if (fz[v]) {
+          for (int w = 0; w < W; ++w) {
+            uint64_t x = fv[w];
+            pc += popc64(x);
+            if (want_fwd)
+              while (x) {
+                my_fwd[w * 64 + __builtin_ctzll(x)] += dl;
+                x &= x - 1;
+              }
           }
         }
+        if (pc) {
+          s_sends += pc * (int64_t)dl;
+          s_active++;
+        }
+        uint64_t* nx = next + (size_t)v * W;
+        fz_next[v] = 0;
+        if (state[v] & ST_DOWN) {
+          memset(nx, 0, (size_t)W * 8);
+          continue;
+        }
+        int64_t newc = 0;
+        uint64_t acc[64];
+        for (int w = 0; w < W; ++w) acc[w] = 0;
+        for (int64_t j = row_ptr[v]; j < row_ptr[v + 1]; ++j) {
+          if (!fz[col[j]]) continue;
+          const uint64_t* fu = front + (size_t)col[j] * W;
+          for (int w = 0; w < W; ++w) acc[w] |= fu[w];
+        }
+        for (int w = 0; w < W; ++w) {
+          uint64_t nw = acc[w] & ~seen[(size_t)v * W + w];
+          nx[w] = nw;
+          if (!nw) continue;
+          seen[(size_t)v * W + w] |= nw;
+          newc += popc64(nw);
+          digest[v] ^= or_term((uint32_t)(r + 1), (uint32_t)w, nw);
+          if (first_out) {
+            uint64_t x = nw;
+            while (x) {
+              int b = __builtin_ctzll(x);
+              first_out[(size_t)v * m + w * 64 + b] = (uint8_t)(r + 1);
+              x &= x - 1;
+            }
+          }
+        }
+        fz_next[v] = newc > 0;
+        s_new += newc;
+        s_recv += newc > 0;
       }
-      s_new += newc;
-      s_recv += newc > 0;
     }
+    if (want_fwd)
+      for (int t = 0; t < nth; ++t)
+        for (int k = 0; k < W * 64; ++k) {
+          fwd[k] += acc_t[(size_t)t * W * 64 + k];
+          acc_t[(size_t)t * W * 64 + k] = 0;
+        }
     st.new_bits = s_new;
     st.receivers = s_recv;
     st.sends = s_sends;
@@ -341,20 +373,42 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
     uint64_t* t = front;
     front = next;
     next = t;
+    uint8_t* tz = fz;
+    fz = fz_next;
+    fz_next = tz;
     rounds = r + 1;
     if (s_new == 0 && r >= last_inject) break;
   }
   if (seen_out) memcpy(seen_out, seen, (size_t)n * W * 8);
   if (digest_out) memcpy(digest_out, digest, (size_t)n * 8);
-  if (coverage_out) {
-    for (int32_t k = 0; k < m; ++k) coverage_out[k] = 0;
-    for (int64_t v = 0; v < n; ++v)
-      for (int32_t k = 0; k < m; ++k) coverage_out[k] += (seen[(size_t)v * W + (k >> 6)] >> (k & 63)) & 1;
+  if (coverage_out) {   /* holders of each message: thread-local counts over vertex blocks */
+#pragma omp parallel
+    {
+      int tid = 0;
+#ifdef _OPENMP
+      tid = omp_get_thread_num();
+#endif
+      uint64_t* my = acc_t + (size_t)tid * W * 64;
+#pragma omp for schedule(static)
+      for (int64_t v = 0; v < n; ++v)
+        for (int w = 0; w < W; ++w) {
+          uint64_t x = seen[(size_t)v * W + w];
+          while (x) {
+            my[w * 64 + __builtin_ctzll(x)]++;
+            x &= x - 1;
+          }
+        }
+    }
+    for (int32_t k = 0; k < m; ++k) {
+      uint64_t c = 0;
+      for (int t = 0; t < nth; ++t) c += acc_t[(size_t)t * W * 64 + k];
+      coverage_out[k] = c;
+    }
   }
   if (forwards_out)
     for (int32_t k = 0; k < m; ++k) forwards_out[k] = fwd[k];
   if (n_reports_out) *n_reports_out = nrep;
   free(front); free(next); free(seen); free(digest); free(state); free(miss);
-  free(deg_live); free(cand); free(fwd);
+  free(deg_live); free(cand); free(fwd); free(fz); free(fz_next); free(acc_t);
   return rounds;
 }

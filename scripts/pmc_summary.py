@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Per-dispatch HBM traffic of k_expand from two rocprofv3 --pmc passes
+"""Per-launch HBM traffic of the pull (k_expand / k_expand_flat and the hub
+passes k_hub_partial / k_hub_final that follow it: the kernel set the bench
+line's roofline and the engine's kernel_ms cover) from two rocprofv3 --pmc passes
 (FETCH_SIZE and WRITE_SIZE in KB; they cannot share a pass on gfx950) next to
 the algorithmic bytes of the same rounds (bench.round_bytes).
 
@@ -18,15 +20,27 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
+SET = ("k_expand", "k_hub_partial", "k_hub_final")
+
+
 def load(d, counter):
+    """Counter per pull launch: a k_expand* dispatch opens a launch, the hub
+    dispatches after it (before the next k_expand*) add to it."""
     path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-    per = {}
+    per, kind = {}, {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "k_expand" not in r["Kernel_Name"]:
+        if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in SET):
             continue
         k = int(r["Dispatch_Id"])
         per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
-    return [per[k] for k in sorted(per)]
+        kind[k] = "k_expand" in r["Kernel_Name"]
+    out = []
+    for k in sorted(per):
+        if kind[k]:
+            out.append(per[k])
+        elif out:
+            out[-1] += per[k]
+    return out
 
 
 def main():
@@ -55,7 +69,7 @@ def main():
     th = sum(x["fetch_GB"] + x["write_GB"] for x in rows)
     tm = sum(x["kernel_ms"] for x in rows)
     print(f"| all {len(rows)} launches | {ta:.2f} | | | {th:.2f} | {th / ta:.3f} | {tm:.2f} | {th / tm:.2f} |")
-    out = {"kernel": "k_expand", "launches": len(rows), "traffic_bytes_per_launch": th * 1e9 / len(rows),
+    out = {"kernel": "k_expand + k_hub_partial + k_hub_final", "launches": len(rows), "traffic_bytes_per_launch": th * 1e9 / len(rows),
            "alg_bytes_per_launch": ta * 1e9 / len(rows), "kernel_ms_per_launch": tm / len(rows),
            "rounds": rows, "config": bench["config"],
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bytes = "

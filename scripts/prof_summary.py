@@ -34,8 +34,28 @@ def main():
     print(f"# {title}\n")
     print("| kernel | calls | total ms | avg us | % |")
     print("|---|---|---|---|---|")
-    for name, calls, tot, avg, pct in rows_from(path):
+    rows = rows_from(path)
+    for name, calls, tot, avg, pct in rows:
         print(f"| `{short(name)}` | {calls} | {tot / 1e6:.3f} | {avg / 1e3:.1f} | {pct:.2f} |")
+    # the bench line's roofline kernel set: the pull launch (k_expand /
+    # k_expand_flat of width W) plus its hub passes, per pull launch -- what
+    # the engine's kernel_ms HIP events bracket
+    sets = {}
+    for name, calls, tot, avg, pct in rows:
+        m = re.search(r"k_(expand_flat|expand|hub_partial|hub_final)<(\d+)", short(name))
+        if not m:
+            continue
+        e = sets.setdefault(m.group(2), {"launches": 0, "pull_ms": 0.0, "hub_ms": 0.0})
+        if m.group(1).startswith("expand"):
+            e["launches"] += calls
+            e["pull_ms"] += tot / 1e6
+        else:
+            e["hub_ms"] += tot / 1e6
+    for w, e in sorted(sets.items()):
+        if e["launches"]:
+            print(f"\nroofline kernel set, W = {w}: k_expand* + k_hub_partial + k_hub_final = "
+                  f"{e['pull_ms']:.3f} + {e['hub_ms']:.3f} ms over {e['launches']} pull launches = "
+                  f"{(e['pull_ms'] + e['hub_ms']) / e['launches']:.3f} ms per launch")
 
 
 if __name__ == "__main__":

@@ -72,6 +72,15 @@ def test_partition_bounds(pkg):
         assert all(b[i][1] == b[i + 1][0] for i in range(p - 1))
         s = (n + p - 1) // p
         assert all(e - s0 <= s for s0, e in b)
+    # arc-balanced slices: each holds about nnz / p in-arcs
+    g = pkg.overlay.barabasi_albert(5000, 3, seed=2)
+    deg = np.diff(g.row_ptr)
+    for p in (2, 3, 8):
+        b = d.partition_bounds(g.n, p, g.row_ptr)
+        assert b[0][0] == 0 and b[-1][1] == g.n
+        assert all(b[i][1] == b[i + 1][0] for i in range(p - 1))
+        arcs = [int(g.row_ptr[e] - g.row_ptr[s0]) for s0, e in b]
+        assert max(arcs) <= g.nnz / p + deg.max()
 
 
 def _shard_worker(rank, world, port, q):

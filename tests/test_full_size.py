@@ -4,18 +4,25 @@ C4: 2^24-vertex Chung-Lu overlay (gamma 2.5, mean degree 16, seed 4), 4096
 messages.  C5: the C4 recipe at 2^26 vertices (seed 5) with 1 %/round crashes,
 3-miss liveness detection and seed removal (Peer.py:298-313, Seed.py:358-406).
 
-The oracle (oracle/gossip_oracle.c, OpenMP) runs message word 0 -- messages
-[0, 64) -- on the overlay the device built; the engine runs the same 64
-messages as a one-word message shard, and every output must be equal: per-round
-counters, Message-Lists, digests, per-message coverage and forwards and (C5)
-the dead-node reports of every round.  The whole 4096-message run (W = 64,
-the bench's configuration) is then tied to that pinned shard through the
-message-shard composition of DESIGN.md §6: shards [0,64) [64,512) [512,1024)
-[1024,2048) [2048,4096) -- widths 1, 8, 8, 16 and 32 words, i.e. the flat
-edge-parallel kernel and the per-receiver kernel -- must add up to the W = 64
-run exactly (per-round new bits / sends / injections, coverage and forwards
-concatenate, digests XOR).  Messages never interact, so this composition is
-an identity of the semantics, not of the implementation.
+C4: the oracle (oracle/gossip_oracle.c, OpenMP) runs ALL 4096 messages (W = 64,
+the bench's configuration) on the overlay the device built, and the engine's
+whole run must equal it output for output: per-round counters, the Message-List
+of every vertex, digests, per-message coverage and forwards.  The receive /
+forward logic restated is Peer.py:175-216, 395-408 plus forward-once
+(DESIGN.md §2).
+
+C5: the oracle runs message word 0 -- messages [0, 64) -- and the last word --
+[4032, 4096) -- each as a one-word run, against the engine's one-word runs of
+the same messages (every counter, digests, coverage, forwards and every round's
+dead-node reports).
+
+Both: the whole 4096-message run is also tied to message shards through the
+composition of DESIGN.md §6: shards [0,64) [64,512) [512,1024) [1024,2048)
+[2048,4096) -- widths 1, 8, 8, 16 and 32 words, i.e. the flat edge-parallel
+kernel and the per-receiver kernel -- must add up to the W = 64 run exactly
+(per-round new bits / sends / injections, coverage and forwards concatenate,
+digests XOR).  Messages never interact, so this composition is an identity of
+the semantics, not of the implementation.
 
 The overlay's degree distribution is also checked.
 """
@@ -77,6 +84,28 @@ def _run(eng, with_reports=False, report_cap=1 << 24):
     return stats, fps
 
 
+def _check_word(part, ref, w_fps=None):
+    """A one-word engine run (counters, Message-Lists when read, digest,
+    coverage, forwards, per-round report fingerprints) against the oracle's."""
+    assert len(part["stats"]) == ref["rounds"]
+    for a, b in zip(part["stats"], ref["stats"]):
+        for k in STAT_KEYS:
+            assert a[k] == b[k], (k, a["round"], a[k], b[k])
+    if "seen" in part:
+        assert np.array_equal(part["seen"], ref["seen"][:, :1])
+    assert np.array_equal(part["digest"], ref["digest"])
+    assert np.array_equal(part["cov"], ref["coverage"])
+    assert np.array_equal(part["fwd"], ref["forwards"])
+    if part["fps"]:
+        assert ref["n_reports"] <= 1 << 27
+        rep = ref["reports"]
+        for r, fp in enumerate(part["fps"]):
+            assert fp == report_fingerprint(rep[rep[:, 2] == r]), r
+        if w_fps is not None:   # liveness is replicated: the same reports every round
+            k = min(len(part["fps"]), len(w_fps))
+            assert k >= 4 and part["fps"][:k] == w_fps[:k]
+
+
 def _full_size(pkg, oracle, log2n, seed, churn):
     n, m = 1 << log2n, 4096
     cfg = dict(track_digest=1)
@@ -101,6 +130,7 @@ def _full_size(pkg, oracle, log2n, seed, churn):
     whole.reset()
     w_stats, w_fps = _run(whole, with_reports=churn)
     w_dig, w_cov, w_fwd = whole.digest().copy(), whole.coverage(), whole.forwards()
+    w_seen = whole.seen() if not churn else None   # 8 GiB at C4
     whole.close()
     _log(f"whole run: {len(w_stats)} rounds in {time.time() - t0:.1f} s")
     assert sum(s["sends"] for s in w_stats) == int(w_fwd.sum())
@@ -123,27 +153,32 @@ def _full_size(pkg, oracle, log2n, seed, churn):
         _log(f"shard [{lo},{hi}) W={sh.words}: {len(stats)} rounds in {time.time() - t0:.1f} s")
     sh.close()
 
-    # shard [0, 64) against the oracle
-    t0 = time.time()
-    ref = oracle.run(g, origin[:64], nthreads=_threads(), want_first=False, report_cap=1 << 27, **okw)
-    _log(f"oracle: {ref['rounds']} rounds in {time.time() - t0:.1f} s ({_threads()} threads)")
-    p0 = parts[0]
-    assert len(p0["stats"]) == ref["rounds"]
-    for a, b in zip(p0["stats"], ref["stats"]):
-        for k in STAT_KEYS:
-            assert a[k] == b[k], (k, a["round"], a[k], b[k])
-    assert np.array_equal(p0["seen"], ref["seen"][:, :1])
-    assert np.array_equal(p0["digest"], ref["digest"])
-    assert np.array_equal(p0["cov"], ref["coverage"])
-    assert np.array_equal(p0["fwd"], ref["forwards"])
-    if churn:
-        assert ref["n_reports"] <= 1 << 27
-        rep = ref["reports"]
-        for r, fp in enumerate(p0["fps"]):
-            assert fp == report_fingerprint(rep[rep[:, 2] == r]), r
-        k = min(len(p0["fps"]), len(w_fps))   # liveness is replicated: the same reports every round
-        assert k >= 4 and p0["fps"][:k] == w_fps[:k]
-        assert sum(s["removals"] for s in w_stats) > 0
+    if not churn:
+        # the whole W = 64 run against the oracle's run of all 4096 messages
+        t0 = time.time()
+        ref = oracle.run(g, origin, nthreads=_threads(), want_first=False)
+        _log(f"oracle, all {m} messages: {ref['rounds']} rounds in {time.time() - t0:.1f} s ({_threads()} threads)")
+        assert len(w_stats) == ref["rounds"]
+        for a, b in zip(w_stats, ref["stats"]):
+            for k in STAT_KEYS:
+                assert a[k] == b[k], (k, a["round"], a[k], b[k])
+        assert w_seen.shape == ref["seen"].shape
+        for lo in range(0, n, 1 << 20):   # blockwise: no 8 GiB temporaries
+            assert np.array_equal(w_seen[lo:lo + (1 << 20)], ref["seen"][lo:lo + (1 << 20)]), lo
+        assert np.array_equal(w_dig, ref["digest"])
+        assert np.array_equal(w_cov, ref["coverage"])
+        assert np.array_equal(w_fwd, ref["forwards"])
+        p0 = parts[0]   # shard [0, 64): its own columns of the oracle's run
+        assert np.array_equal(p0["seen"], ref["seen"][:, :1])
+        assert np.array_equal(p0["cov"], ref["coverage"][:64])
+        assert np.array_equal(p0["fwd"], ref["forwards"][:64])
+        del ref, w_seen
+    else:
+        # one-word runs of the first and the last message word against the oracle
+        ref = oracle.run(g, origin[:64], nthreads=_threads(), want_first=False, report_cap=1 << 27, **okw)
+        _log(f"oracle, word 0: {ref['rounds']} rounds ({_threads()} threads)")
+        _check_word(parts[0], ref, w_fps)
+        del ref
 
     # the whole run is the composition of the shards
     R = len(w_stats)
@@ -159,33 +194,35 @@ def _full_size(pkg, oracle, log2n, seed, churn):
     assert np.array_equal(dig, w_dig)
     assert np.array_equal(np.concatenate([p["cov"] for p in parts]), w_cov)
     assert np.array_equal(np.concatenate([p["fwd"] for p in parts]), w_fwd)
-    return dict(stats=w_stats, cov=w_cov, fwd=w_fwd, g=g, origin=origin, cfg=cfg)
+    return dict(stats=w_stats, cov=w_cov, fwd=w_fwd, g=g, origin=origin, cfg=cfg, fps=w_fps)
 
 
 @pytest.mark.timeout(900)
 def test_c4_full_size_parity(pkg, oracle):
-    """BASELINE config 4 at its own size: 2^24 vertices x 4096 messages."""
+    """BASELINE config 4 at its own size: 2^24 vertices x 4096 messages, the
+    whole W = 64 run against the oracle's run of all 4096 messages."""
     out = _full_size(pkg, oracle, 24, 4, churn=False)
     assert out["stats"][-1]["new_bits"] == 0
-    # a second pinned word, the last one: messages [4032, 4096) alone vs the oracle
-    # and vs the whole run's columns
-    with pkg.GossipEngine(0, **out["cfg"]) as eng:
-        eng.load_graph(out["g"])
-        eng.configure(msg_word_base=0)   # local word numbers, as the oracle's digest
-        eng.set_messages(out["origin"][4032:])
-        eng.reset()
-        stats, _ = _run(eng)
-        dig, cov, fwd = eng.digest(), eng.coverage(), eng.forwards()
-    ref = oracle.run(out["g"], out["origin"][4032:], nthreads=_threads())
-    assert [s["new_bits"] for s in stats] == [s["new_bits"] for s in ref["stats"]]
-    assert [s["sends"] for s in stats] == [s["sends"] for s in ref["stats"]]
-    assert np.array_equal(cov, ref["coverage"]) and np.array_equal(cov, out["cov"][4032:])
-    assert np.array_equal(fwd, ref["forwards"]) and np.array_equal(fwd, out["fwd"][4032:])
-    assert np.array_equal(dig, ref["digest"])
 
 
 @pytest.mark.timeout(1200)
 def test_c5_full_size_parity(pkg, oracle):
     """BASELINE config 5 at its own size: 2^26 vertices x 4096 messages, 1 %/round
     crashes, 3-miss detection, seed removal."""
-    _full_size(pkg, oracle, 26, 5, churn=True)
+    out = _full_size(pkg, oracle, 26, 5, churn=True)
+    assert sum(s["removals"] for s in out["stats"]) > 0
+    # the last message word, [4032, 4096), alone against the oracle and against
+    # the whole run's columns
+    with pkg.GossipEngine(0, **out["cfg"]) as eng:
+        eng.load_graph(out["g"])
+        eng.configure(msg_word_base=0)   # local word numbers, as the oracle's digest
+        eng.set_messages(out["origin"][4032:])
+        eng.reset()
+        stats, fps = _run(eng, with_reports=True)
+        part = dict(stats=stats, fps=fps, digest=eng.digest().copy(), cov=eng.coverage(), fwd=eng.forwards())
+    ref = oracle.run(out["g"], out["origin"][4032:], nthreads=_threads(), want_first=False, report_cap=1 << 27,
+                     churn=True, p_fail=0.01, churn_seed=5)
+    _log(f"oracle, last word: {ref['rounds']} rounds")
+    _check_word(part, ref, out["fps"])
+    assert np.array_equal(part["cov"], out["cov"][4032:])
+    assert np.array_equal(part["fwd"], out["fwd"][4032:])

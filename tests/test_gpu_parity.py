@@ -282,11 +282,14 @@ def _group_run(pkg, g, origin, inject, P, crashes=(), **cfg):
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
 @pytest.mark.parametrize("churn", [False, True])
-def test_group_partition_invariance(pkg, oracle, mode, churn):
+@pytest.mark.parametrize("by_arcs", [0, 1], ids=["vertex-slices", "arc-slices"])
+def test_group_partition_invariance(pkg, oracle, mode, churn, by_arcs):
     """Vertex partition over P = 2, 3, 4 contexts: owned
-    slices + ghost rows, the sparse boundary exchange of this round's new
-    bits (and removal flags) through the same pack / unpack buffers as the
-    RCCL path.  Every output equals the oracle's (one context)."""
+    slices (equal vertex counts, or equal arc counts) + ghost
+    rows, the sparse boundary exchange of this round's new bits (and removal
+    flags) through the same pack / unpack buffers and the same exchange plan
+    (csrc/xplan.h) as the RCCL path.  Every output equals the oracle's (one
+    context)."""
     push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
     origin = pkg.overlay.random_origins(g.n, 200, seed=8)
@@ -295,11 +298,13 @@ def test_group_partition_invariance(pkg, oracle, mode, churn):
     crashes = [(int(origin[5]), 1), (17, 2)] if churn else []
     ref = oracle.run(g, origin, inject, crashes=crashes, want_first=True, **kw)
     cfg = dict(track_first=1, track_msg_forwards=int(churn), push_ratio=push_ratio, unfiltered_pct=unfiltered_pct,
-               flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
+               flat_max_words=flat_max_words, arc_mask_permille=arc_mask, partition_by_arcs=by_arcs)
     if churn:
         cfg.update(churn=1, p_fail=0.02, churn_seed=3)
     for P in (2, 3, 4):
         engs, stats, reports = _group_run(pkg, g, origin, inject, P, crashes, **cfg)
+        bounds = pkg.dist.partition_bounds(g.n, P, g.row_ptr if by_arcs else None)
+        assert [e.partition() for e in engs] == bounds
         assert len(stats) == ref["rounds"], P
         for a, b in zip(stats, ref["stats"]):
             for k in STAT_KEYS:
@@ -341,7 +346,8 @@ def test_group_partition_invariance(pkg, oracle, mode, churn):
             e.close()
 
 
-def test_partition_local_graph(pkg):
+@pytest.mark.parametrize("by_arcs", [0, 1], ids=["vertex-slices", "arc-slices"])
+def test_partition_local_graph(pkg, by_arcs):
     """The local CSR of a partition: owned rows are the global in-lists
     (gather order, local ids), ghost rows list their owned neighbours, and
     every rank's ghosts of owner p are exactly the vertices p sends to it."""
@@ -349,17 +355,21 @@ def test_partition_local_graph(pkg):
     P = 3
     origin = np.array([0, 1999, 1000], np.int32)
     locs = []
+    bounds = pkg.dist.partition_bounds(g.n, P, g.row_ptr if by_arcs else None)
     for k in range(P):
-        with pkg.GossipEngine(0) as e:
+        with pkg.GossipEngine(0, partition_by_arcs=by_arcs) as e:
             e.load_graph(g)
             e.set_partition(k, P)
             e.set_messages(origin)
             vb, ve = e.partition()
             rp, col, l2g = e.local_graph()
             locs.append((vb, ve, rp, col, l2g, e.local_info()))
-    S = -(-g.n // P)
+    if by_arcs:   # BA's early vertices are its hubs: arc slices hold fewer of them
+        arcs = [int(g.row_ptr[e] - g.row_ptr[b]) for b, e in bounds]
+        assert max(arcs) - min(arcs) <= int(np.diff(g.row_ptr).max())
+        assert bounds[0][1] - bounds[0][0] < bounds[-1][1] - bounds[-1][0]
     for k, (vb, ve, rp, col, l2g, (nloc, ng, nx, nnz_l, nb)) in enumerate(locs):
-        assert (vb, ve) == (k * S, min(g.n, (k + 1) * S)) and nloc == ve - vb
+        assert (vb, ve) == bounds[k] and nloc == ve - vb
         assert np.array_equal(l2g[:nloc], np.arange(vb, ve))
         ghosts = l2g[nloc:nloc + ng]
         assert np.all(np.diff(ghosts) > 0) and not np.any((ghosts >= vb) & (ghosts < ve))
@@ -402,6 +412,31 @@ def test_rccl_one_rank(pkg, oracle):
         assert np.array_equal(e.digest(), ref["digest"])
         assert np.array_equal(e.coverage(), ref["coverage"])
         assert np.array_equal(e.forwards(), ref["forwards"])
+
+
+def test_asymmetric_overlay_rejected_by_partition(pkg):
+    """A vertex partition relies on the overlay being symmetric (Seed.py:131-149):
+    rank q's ghosts of owner p are then exactly p's send list B_pq.  An
+    asymmetric in-CSR loaded as undirected must be rejected before the first
+    exchange (xplan_check_lists), not unpacked into another owner's ghosts."""
+    arcs = [(0, 1), (1, 0), (5, 6), (6, 5), (2, 7)]   # 2 -> 7 without 7 -> 2
+    src = np.array([a for a, _ in arcs]); dst = np.array([b for _, b in arcs])
+    g = pkg.CSR.from_arcs(10, src, dst, directed=True)
+    g = pkg.CSR(g.n, g.row_ptr, g.col, False)
+    engs = []
+    try:
+        for k in range(2):
+            e = pkg.GossipEngine(0)
+            e.load_graph(g)
+            e.set_partition(k, 2)
+            e.set_messages(np.array([2, 0], np.int32))
+            e.reset()
+            engs.append(e)
+        with pytest.raises(pkg.GossipError, match="not symmetric"):
+            pkg.GossipEngine.round_group(engs)
+    finally:
+        for e in engs:
+            e.close()
 
 
 def test_partitioned_round_needs_an_exchange(pkg):
