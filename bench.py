@@ -59,8 +59,9 @@ def parse():
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--cpu-log2n", type=int, default=20,
-                    help="cpu_baseline: overlay size of the oracle's bounded sample (all messages, W = 64)")
+    ap.add_argument("--cpu-log2n", type=int, default=22,
+                    help="cpu_baseline: overlay size of the oracle's bounded sample (all messages, W = 64); "
+                         "24 times the whole C4 run (about a minute on 16 host threads)")
     ap.add_argument("--parallel", choices=("messages", "vertex"), default="messages",
                     help="N > 1: message shards (no data-path collective, default) or the vertex "
                          "partition with a sparse boundary exchange every round (ncclSend/Recv of "
@@ -147,11 +148,12 @@ def cpu_baseline(args, eng, origin, pkg):
     """Two CPU legs, timed on this box's host cores (reported beside the GPU
     line, never the target):
       port     oracle/gossip_oracle.c (OpenMP, every thread this process may
-               use) running ALL `messages` (W = 64 words per Message-List row,
-               the GPU's layout) to quiescence on a 2^cpu_log2n-vertex overlay
-               of the same Chung-Lu recipe and seed -- a bounded sample of the
-               workload (the whole 2^24 run would take minutes) in the same unit;
-               this leg is `value`;
+               use: OMP_NUM_THREADS, else the affinity set) running ALL
+               `messages` (W = 64 words per Message-List row, the GPU's layout)
+               to quiescence on a 2^cpu_log2n-vertex overlay of the same
+               Chung-Lu recipe and seed -- a bounded sample of the workload
+               (2^22 by default: ~10-20 s on 16 threads; --cpu-log2n 24 times
+               the whole C4 run) in the same unit; this leg is `value`;
       harness  oracle/harness.py, the reference's per-peer Message-List logic
                (sha256 digests in a set per peer, Peer.py:175-216, 395-408) plus
                forwarding, single-core, on BASELINE config 2 (10^4-node BA(m=2),
@@ -177,7 +179,8 @@ def cpu_baseline(args, eng, origin, pkg):
                      f"2^{args.cpu_log2n} vertices ({g.nnz} arcs), all {len(o)} messages (W = 64), full run"
                      f"{' with churn' if churn else ''} ({ref['rounds']} rounds, {sends} edge-deliveries, "
                      f"{dt:.1f} s, {threads} OpenMP threads)",
-           "host": {"nproc": nproc, "affinity": aff, "cpu_model": model}}
+           "host": {"nproc": nproc, "affinity": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+                    "cpu_model": model}}
     # leg 2: the per-peer Python harness, single core, BASELINE config 2
     h = pkg.overlay.barabasi_albert(10000, 2, seed=2)
     ho = pkg.overlay.random_origins(h.n, 64, seed=2).tolist()

@@ -181,7 +181,10 @@ struct ExpandArgs {
   int32_t early_exit;                  // this round scans with the coverage check
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
   int32_t near_done;                   // early-exit round with most messages held: fewer rows in flight
+  int32_t pairs;                       // unfiltered W = 64 round: the SCAN_PAIRS variant (late rounds)
   const u64* __restrict__ alive;       // [W] messages some sender forwards this round (or null)
+  const u64* __restrict__ wbits;       // alive rounds after k_want: bit v clear = v holds every alive
+                                       //   message of its component, nothing to scan (or null)
   u64* __restrict__ alive_next;        // [W] the same for round r + 1: OR of the new rows (or null)
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
   const u64* __restrict__ cmk;         // record rounds: dense bitmap of this round's senders (bit v:
@@ -211,6 +214,8 @@ struct ExpandArgs {
   const int32_t* __restrict__ ocol;
   u64* __restrict__ acc;               // [n_alloc][W] OR accumulator (all-zero between uses)
   u64* __restrict__ tbits;             // [n_alloc/64] receivers pushed to this round
+  const u64* __restrict__ nbits;       // push rounds of narrow rows: bit v = v can still receive
+                                       //   (owned, up, not done); null: checked per arc
   int32_t* __restrict__ touched;       // receivers touched this round
   const int32_t* __restrict__ active;  // senders with deg <= hub_thr
   const int32_t* __restrict__ big;     // senders with deg > hub_thr
@@ -385,7 +390,9 @@ __device__ __forceinline__ void reduce_slots(u64x2& acc) {
 enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PRE = 3,
                 SCAN_CML = 4 /* flag: read / write compact Message-Lists (W = 64) */,
                 SCAN_ALIVE = 8 /* flag: early-exit targets narrowed to the alive messages (k_expand);
-                                  a variant of its own: +2-3 VGPRs cost a wave per SIMD */ };
+                                  a variant of its own: +2-3 VGPRs cost a wave per SIMD */,
+                SCAN_PAIRS = 16 /* flag: receivers with short in-lists two at a time (short_pairs,
+                                   W = 64), a variant of its own for the late latency-bound rounds */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
@@ -1023,7 +1030,8 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
   const int g = lane / LPR, lw = lane % LPR;
   auto& L = s_w[wib];
   constexpr bool ALIVE = (MODE & SCAN_ALIVE) != 0;
-  constexpr int SCAN = MODE & ~SCAN_ALIVE;
+  constexpr bool PAIRS = (MODE & SCAN_PAIRS) != 0;
+  constexpr int SCAN = MODE & ~(SCAN_ALIVE | SCAN_PAIRS);
   WaveStats st;
   ws_zero(st);
   const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
@@ -1043,6 +1051,9 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       if (lane == 63 || li + 1 == a.nloc) L.rp[lane + 1] = e;
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
       need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
+      if constexpr (ALIVE) {   // k_want found that v wants no alive message (its 64-vertex word)
+        if (need && a.wbits) need = ((a.wbits[li >> 6] >> lane) & 1ull) != 0ull;
+      }
       if constexpr ((MODE & 3) == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
       if constexpr ((MODE & 3) == SCAN_PRE) {
         // sparse filtered rounds: every lane probes the in-list of its own
@@ -1167,7 +1178,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         m &= ~mp;
       }
     }
-    if constexpr (GP_SHORT_PAIRS && W == 64 && (MODE & 3) != SCAN_MASKED) {
+    if constexpr ((GP_SHORT_PAIRS || PAIRS) && W == 64 && (MODE & 3) != SCAN_MASKED) {
       bool pairs = true;   // (record rounds read records in the single-receiver scan)
       if constexpr ((MODE & SCAN_CML) != 0) pairs = a.cmk == nullptr;
       if (pairs) {   // receivers with short in-lists two at a time, the rest below
@@ -1213,6 +1224,92 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     }
     alive_flush<W>(a, L.alive, lane);
     commit_vertices(a, L, li, need, st);
+  }
+  flush_stats(st, a.partial);
+}
+
+// ---------------------------------------------------------------------------
+// Alive-set pre-check (churn): late early-exit rounds under
+// liveness leave most vertices incomplete for good -- crashes cut some of
+// their component's messages off -- while they already hold every message
+// anyone still forwards (F_r).  The serial loop of k_expand finds that out
+// one receiver at a time (seen row, component mask, then nothing to scan: a
+// dependent chain per vertex, C5 round 6: 62 M of them for 1.3 M receivers).
+// k_want runs the same test, want = cmask & F_r & ~seen, for a wave's 64
+// vertices with Q x RPI rows in flight, and clears the bit of every vertex
+// that wants nothing; k_expand's lane phase then drops those from its serial
+// loop.  Exact: such a vertex would have been skipped there with nothing
+// gathered (acc = 0, no commit).  Vertices this kernel does not check (hubs,
+// no in-arcs, not needy) keep their bit.
+#ifndef GP_WANT_DIV
+#define GP_WANT_DIV 64.0   // pre-check when last round's new bits <= n*m / GP_WANT_DIV (0: never)
+#endif
+// (the environment variable GP_WANT_DIV overrides it: the parity suite runs
+// the alive rounds with the pre-check forced on and off)
+static double want_div() {
+  const char* e = getenv("GP_WANT_DIV");
+  return e && *e ? atof(e) : GP_WANT_DIV;
+}
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_want(ExpandArgs a, u64* __restrict__ wbits) {
+  constexpr int LPR = Geo<W>::LPR;
+  constexpr int RPI = Geo<W>::RPI;
+  constexpr int Q = 4;   // row wave-instructions in flight (seen + mask pieces each)
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  WaveStats st;
+  ws_zero(st);
+  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
+  if (base < a.nloc) {
+    const int64_t li = base + lane;
+    bool need = false;
+    uint32_t slot = SLOT_NONE;
+    int32_t mrow = 0;
+    if (li < a.nloc) {
+      const int v = (int)(a.vbegin + li);
+      const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
+      need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && e - b <= a.hub_thr && e > b;
+      if (need) {
+        slot = a.sp[v];
+        mrow = a.midx[v];
+      }
+    }
+    u64 m = __ballot(need);
+    const u64x2 fa = load_piece<W>(a.alive, 0, lw);
+    u64 drop = 0;        // this lane's share of the wave's "wants nothing" bits
+    uint32_t nseen = 0;  // seen rows read (lw == 0 lanes count their vertex)
+    while (m) {
+      const int cnt = __popcll(m);
+      int kk[Q];
+      u64x2 sv[Q], cm[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int t = q * RPI + g;
+        kk[q] = t < cnt ? select_bit(m, t + 1) : -1;
+        const int kq = kk[q] >= 0 ? kk[q] : 0;
+        const uint32_t s = (uint32_t)__shfl((int)slot, kq);
+        const int32_t mr = __shfl(mrow, kq);
+        sv[q] = u64x2{0, 0};
+        cm[q] = u64x2{0, 0};
+        if (kk[q] >= 0) {
+          if (s != SLOT_NONE) sv[q] = load_piece<W>(a.slot[s], a.vbegin + base + kq, lw);
+          cm[q] = load_piece<W>(a.cmask, mr, lw);
+          if (lw == 0 && s != SLOT_NONE) ++nseen;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const u64x2 w = cm[q] & fa & ~sv[q];
+        const bool any = group_or<LPR>((w.x | w.y) != 0ull);
+        if (kk[q] >= 0 && !any && lw == 0) drop |= 1ull << kk[q];
+      }
+      for (int i = 0; i < Q * RPI && m; ++i) m &= m - 1;   // the vertices just checked
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) drop |= __shfl_xor(drop, o);
+    st.add(S_SEEN_READ, (u64)wave_sum_u32(nseen));
+    if (lane == 0) wbits[base >> 6] = ~drop;
   }
   flush_stats(st, a.partial);
 }
@@ -1698,8 +1795,10 @@ __device__ __forceinline__ void push_arcs(const ExpandArgs& a, int64_t jb, int64
       const int64_t j = t / nnz;
       const int q = (int)(t - j * nnz);
       v = a.ocol[jb + j];
-      if (v >= a.vbegin && v < a.vbegin + a.nloc && !(a.state[v] & ST_DOWN) &&
-          a.seenpop[v - a.vbegin] < a.done_at[v]) {
+      const bool recv = a.nbits ? ((a.nbits[v >> 6] >> (v & 63)) & 1ull) != 0ull
+                                : (v >= a.vbegin && v < a.vbegin + a.nloc && !(a.state[v] & ST_DOWN) &&
+                                   a.seenpop[v - a.vbegin] < a.done_at[v]);
+      if (recv) {
         const int w = swords[q];
         atomicOr(&a.acc[(size_t)v * W + w], srow[w]);
         if (q == 0) atomicOr(&a.tbits[v >> 6], 1ull << (v & 63));
@@ -1845,6 +1944,121 @@ __global__ __launch_bounds__(BLOCK) void k_apply(ExpandArgs a) {
     finish_row<W, false, false>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
   }
   alive_flush<W>(a, s_w[wib].alive, lane);
+  flush_stats(st, a.partial);
+}
+
+// receivable bitmap of a narrow push round: bit v = v is owned, up and not
+// done, i.e. the per-arc test of push_arcs done once per vertex (2 MB at 2^24,
+// L2-resident, instead of three scattered loads per arc)
+__global__ __launch_bounds__(BLOCK) void k_mkneed(const uint8_t* __restrict__ state,
+                                                  const uint32_t* __restrict__ seenpop,
+                                                  const uint32_t* __restrict__ done_at, int64_t vbegin,
+                                                  int64_t nloc, int64_t n, u64* __restrict__ nbits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
+    const int64_t v = v0 + lane;
+    bool ok = false;
+    if (v >= vbegin && v < vbegin + nloc) ok = !(state[v] & ST_DOWN) && seenpop[v - vbegin] < done_at[v];
+    const u64 m = __ballot(ok);
+    if (lane == 0) nbits[v0 >> 6] = m;
+  }
+}
+
+// receiver side of a narrow push round, lane-parallel: a wave takes 64
+// touched receivers (the touched list is in vertex order within a block) and
+// runs them RPI per wave-instruction with LPR lanes x 16 B per row, like the
+// flat pull's receiver side; per-receiver words are committed one receiver
+// per lane.  Same results as k_apply (finish_row), which spends a whole wave
+// on each receiver: at W <= 32 most of its lanes idle.
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_apply_lanes(ExpandArgs a) {
+  constexpr int LPR = Geo<W>::LPR;
+  constexpr int RPI = Geo<W>::RPI;
+  constexpr int WPL = Geo<W>::WPL;
+  struct ApplyLds {
+    uint32_t tot[64];
+    u64 dig[64];
+    int8_t rd[64];
+    u64 alive[W];
+  };
+  __shared__ ApplyLds s_a[WAVES];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  ApplyLds& L = s_a[wib];
+  WaveStats st;
+  ws_zero(st);
+  const int64_t nt = (int64_t)a.stats[S_TOUCH_CURSOR];
+  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
+  if (base < nt) {
+    alive_zero<W>(a, L.alive, lane);
+    const bool mine = base + lane < nt;
+    const int v = mine ? a.touched[base + lane] : 0;
+    const uint32_t slot_of = mine ? (uint32_t)a.sp[v] : SLOT_NONE;
+    st.add(S_VISITED, (u64)__popcll(__ballot(mine)));
+    wave_sync_lds();
+    for (int r0 = 0; r0 < 64; r0 += RPI) {
+      const int r = r0 + g;
+      const int rv = __shfl(v, r);
+      const uint32_t rslot = (uint32_t)__shfl((int)slot_of, r);
+      const bool rn = base + r < nt;
+      u64x2 acc = {0, 0};
+      if (rn) {
+        acc = load_piece<W>(a.acc, rv - a.vbegin, lw);
+        store_piece<W>(a.acc, rv - a.vbegin, lw, u64x2{0, 0});   // the accumulator stays all-zero
+      }
+      const bool any = group_or<LPR>((acc.x | acc.y) != 0ull);
+      u64x2 sv = {0, 0};
+      if (any && rslot != SLOT_NONE) sv = load_piece<W>(a.slot[rslot], rv, lw);
+      const u64x2 nw = acc & ~sv;
+      const uint32_t tot = group_sum<LPR>((uint32_t)(__popcll(nw.x) + __popcll(nw.y)));
+      u64 t = 0;
+      if (tot) {
+        alive_add<W>(a, L, lw, nw);
+        store_piece<W>(a.slot[a.wslot], rv, lw, sv | nw);
+        if (a.frx_next) store_piece<W>(a.frx_next, rv, lw, nw);
+        if (a.first) {
+          uint8_t* row = a.first + (size_t)(rv - a.vbegin) * (W * 64);
+          if (nw.x) set_first_bytes(row, lw * WPL, nw.x, (uint32_t)a.rr);
+          if (WPL == 2 && nw.y) set_first_bytes(row, lw * WPL + 1, nw.y, (uint32_t)a.rr);
+        }
+        if (a.digest) {
+          if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + lw * WPL), nw.x);
+          if (WPL == 2 && nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + lw * WPL + 1), nw.y);
+        }
+      }
+      t = group_xor<LPR>(t);
+      if (lw == 0) {
+        L.tot[r] = tot;
+        L.dig[r] = t;
+        L.rd[r] = (int8_t)(any && rslot != SLOT_NONE);
+      }
+    }
+    wave_sync_lds();
+    u64 nbits = 0, nrecv = 0, narcs = 0, nseen = 0;
+    if (mine) {
+      const uint32_t tot = L.tot[lane];
+      nseen = (u64)L.rd[lane];
+      if (tot) {   // (fpop_next of the owned vertices was zeroed before the push)
+        const int64_t i = v - a.vbegin;
+        a.fpop_next[v] = tot;
+        a.seenpop[i] += tot;
+        a.sp[v] = (uint8_t)a.wslot;
+        a.ws[v] |= (uint8_t)(1u << a.wslot);
+        if (a.digest) a.digest[i] ^= L.dig[lane];
+        nbits = tot;
+        nrecv = 1;
+        narcs = (u64)(uint32_t)max(a.deg_live[v], 0);
+      }
+    }
+    st.add(S_NEW_BITS, wave_sum_u64(nbits));
+    st.add(S_RECEIVERS, wave_sum_u64(nrecv));
+    st.add(S_WRITTEN, wave_sum_u64(nrecv));
+    st.add(S_NEXT_ARCS, wave_sum_u64(narcs));
+    st.add(S_SEEN_READ, wave_sum_u64(nseen));
+    alive_flush<W>(a, L.alive, lane);
+  }
   flush_stats(st, a.partial);
 }
 
@@ -2793,17 +3007,33 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.stats = c->d_stats;
 }
 
+// narrow rows (W <= GP_PUSH_LANES_MAXW): the receivable bitmap and the
+// lane-parallel receiver side (k_mkneed, k_apply_lanes)
+#ifndef GP_PUSH_LANES_MAXW
+#define GP_PUSH_LANES_MAXW 32
+#endif
 template <int W>
 static void launch_push_w(Ctx* c, ExpandArgs a) {
   hipStream_t s = c->stream;
   const int64_t nwords = (c->n_alloc + 63) / 64;
+  constexpr bool lanes = W <= GP_PUSH_LANES_MAXW;
+  if (lanes) {
+    hipLaunchKernelGGL(k_mkneed, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
+                       dim3(BLOCK), 0, s, c->d_state, c->d_seenpop, c->d_done_at, a.vbegin, a.nloc, c->n_alloc,
+                       c->d_nbits);
+    a.nbits = c->d_nbits;
+  }
   hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_abits, nwords,
                      a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats);
   hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_touch_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_tbits, nwords,
                      c->d_touched, c->d_stats);
-  hipLaunchKernelGGL(k_apply<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
+  if (lanes)   // one wave per 64 touched receivers; the grid covers every vertex
+    hipLaunchKernelGGL(k_apply_lanes<W>, dim3(grid_for(std::max<int64_t>(c->nloc(), 1), (int64_t)WAVES * 64)),
+                       dim3(BLOCK), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_apply<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
 }
 
 template <int W>
@@ -2842,6 +3072,16 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   }
   const int mode = a.unfiltered ? SCAN_UNFILTERED : SCAN_FILTERED;
   (void)hipEventRecord(c->ev[4], c->stream);
+  // alive-set pre-check (k_want) ahead of the per-receiver kernel's alive variants
+  if constexpr (W >= 32) {
+    if (a.wbits && !flat && a.alive && a.early_exit && a.nloc > 0)
+      hipLaunchKernelGGL(k_want<W>, dim3(grid_for(a.nloc, per_block)), dim3(BLOCK), 0, c->stream, a,
+                         const_cast<u64*>(a.wbits));
+    else
+      a.wbits = nullptr;
+  } else {
+    a.wbits = nullptr;
+  }
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
     const dim3 grid(grid_for(a.nloc, (int64_t)WAVES * FlatNR<W>::value));
     if constexpr (W <= 32) {
@@ -2861,8 +3101,14 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     if (alive_ee) {
       if constexpr (W >= 32)
         hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
-    } else if (mode == SCAN_UNFILTERED)
-      hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+    } else if (mode == SCAN_UNFILTERED) {
+      bool pairs = false;   // late near-done rounds: short in-lists two receivers at a time
+      if constexpr (W == 64) pairs = a.pairs != 0;
+      if constexpr (W == 64) {
+        if (pairs) hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_PAIRS>), grid, dim3(BLOCK), 0, c->stream, a);
+      }
+      if (!pairs) hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+    }
     else if (masked)
       hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(BLOCK), 0, c->stream, a);
     else if (W == 64 && (a.cmk || a.cmk_next)) {   // compact Message-Lists read and / or written
@@ -2932,7 +3178,13 @@ static int launch_expand(Ctx* c) {
                        (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m);
   const u64 inj = (size_t)r < c->inj_arcs.size() ? (u64)c->inj_arcs[(size_t)r] : 0ull;
   const double est = (double)((r == 0 ? 0ull : c->prev_next_arcs) + inj);
-  c->mode_push = c->cfg.push_ratio > 0.0 && est * c->cfg.push_ratio <= (double)c->nnz;
+  // narrow rows push at a lower ratio: the pull's per-arc scan does not
+  // shrink with W, the push's row words do (k_apply_lanes, k_mkneed)
+#ifndef GP_NARROW_PUSH_SCALE
+#define GP_NARROW_PUSH_SCALE 1.0
+#endif
+  const double ratio = c->cfg.push_ratio * (c->words <= 16 ? GP_NARROW_PUSH_SCALE : 1.0);
+  c->mode_push = c->cfg.push_ratio > 0.0 && est * ratio <= (double)c->nnz;
   if (c->mode_push && c->nloc() > 0)
     GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1], 0, (size_t)c->nloc() * 4, c->stream));
   // unfiltered pull when (nearly) every vertex is a sender: last round's
@@ -2995,6 +3247,23 @@ static int launch_expand(Ctx* c) {
   // C5 rounds 5-6 56.8 -> 64.3 ms with the switch on)
   a.near_done = c->early_exit_now && !c->liveness_active &&
                 (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m ? 1 : 0;
+  // paired short in-lists in the late near-done rounds (few new bits last
+  // round: receivers complete after a few rows, the serial chain is the bound)
+#ifndef GP_PAIRS_DIV
+#define GP_PAIRS_DIV 0.0   // SCAN_PAIRS when last round's new bits <= n*m / GP_PAIRS_DIV (0: never)
+#endif
+  a.pairs = GP_PAIRS_DIV > 0.0 && a.near_done && a.unfiltered &&
+            (double)c->prev_new_bits * GP_PAIRS_DIV <= (double)c->n * (double)c->m ? 1 : 0;
+  // alive-set pre-check (k_want): early-exit rounds under liveness once the
+  // rounds have gone sparse (most incomplete vertices already hold every
+  // message still forwarded)
+  a.wbits = nullptr;
+  const double wdiv = want_div();
+  if (wdiv > 0.0 && alive_on(c) && c->early_exit_now && !c->mode_push && c->words >= 32 &&
+      (double)c->prev_new_bits * wdiv <= (double)c->n * (double)c->m) {
+    if (!c->d_wbits) GP_TRY(dalloc(&c->d_wbits, (size_t)(c->n_alloc + 63) / 64 + 1));
+    a.wbits = c->d_wbits;
+  }
   switch (c->words) {
     case 1: launch_expand_w<1>(c, a); break;
     case 2: launch_expand_w<2>(c, a); break;
@@ -3108,8 +3377,8 @@ static void free_state(Ctx* c) {
   dfree(&c->d_det_big); dfree(&c->d_det_pre); dfree(&c->d_det_live); dfree(&c->d_det_cur); dfree(&c->d_det_base);
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
-  dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
-  dfree(&c->d_midx); dfree(&c->d_cmask);
+  dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
+  dfree(&c->d_midx); dfree(&c->d_cmask); dfree(&c->d_wbits);
   bitcount_free(c);
   c->d_msg_fwd = nullptr;
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -3238,6 +3507,7 @@ static int alloc_state(Ctx* c) {
   GP_HIP(hipMemsetAsync(c->d_acc, 0, nl * W * 8, c->stream));
   GP_TRY(dalloc(&c->d_tbits, (na + 63) / 64));
   GP_HIP(hipMemsetAsync(c->d_tbits, 0, (na + 63) / 64 * 8, c->stream));
+  GP_TRY(dalloc(&c->d_nbits, (na + 63) / 64));
   GP_TRY(dalloc(&c->d_touched, na));
   GP_TRY(dalloc(&c->d_active, na));
   GP_TRY(dalloc(&c->d_big, na));
@@ -3400,8 +3670,8 @@ void gp_destroy(gp_ctx* c) {
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
   dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
-  dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
-  dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
+  dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask); dfree(&c->d_wbits);
+  dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
   dfree(&c->d_slot[2]);
   for (int k = 0; k < 2; ++k) { dfree(&c->d_slot[k]); dfree(&c->d_frx[k]); dfree(&c->d_fpop[k]); }

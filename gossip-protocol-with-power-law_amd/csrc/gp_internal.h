@@ -138,6 +138,8 @@ struct Ctx {
   uint32_t* d_det_cur = nullptr;
   u64* d_det_base = nullptr;
   // [n_alloc/64] frontier_r activity bitmap (fpop != 0): 2 MB at 2^24
+  u64* d_nbits = nullptr;           // [n_alloc/64] narrow push rounds: receivable vertices (k_mkneed)
+  u64* d_wbits = nullptr;           // [n_alloc/64] k_want: bit v clear = wants no alive message this round
   u64* d_abits = nullptr;
   u64* d_sbits = nullptr;   // summary level of d_abits (GP_SUMMARY_PROBE builds)
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
