@@ -59,9 +59,9 @@ def parse():
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--cpu-log2n", type=int, default=22,
-                    help="cpu_baseline: overlay size of the oracle's bounded sample (all messages, W = 64); "
-                         "24 times the whole C4 run (about a minute on 16 host threads)")
+    ap.add_argument("--cpu-log2n", type=int, default=None,
+                    help="cpu_baseline: overlay size of the oracle's run (all messages, W = 64); default: the "
+                         "workload's own size up to 2^24 -- the whole C4 run, ~30 s on 16 host threads")
     ap.add_argument("--parallel", choices=("messages", "vertex"), default="messages",
                     help="N > 1: message shards (no data-path collective, default) or the vertex "
                          "partition with a sparse boundary exchange every round (ncclSend/Recv of "
@@ -72,6 +72,8 @@ def parse():
     c5 = a.workload == "c5"
     if a.log2n is None:
         a.log2n = 26 if c5 else 24
+    if a.cpu_log2n is None:   # C4 itself; C5's 2^26 (4x the rows and arcs) is sampled at 2^24
+        a.cpu_log2n = min(a.log2n, 24)
     if a.seed is None:
         a.seed = 5 if c5 else 4
     return a
@@ -151,9 +153,9 @@ def cpu_baseline(args, eng, origin, pkg):
                use: OMP_NUM_THREADS, else the affinity set) running ALL
                `messages` (W = 64 words per Message-List row, the GPU's layout)
                to quiescence on a 2^cpu_log2n-vertex overlay of the same
-               Chung-Lu recipe and seed -- a bounded sample of the workload
-               (2^22 by default: ~10-20 s on 16 threads; --cpu-log2n 24 times
-               the whole C4 run) in the same unit; this leg is `value`;
+               Chung-Lu recipe and seed: by default the workload itself at
+               C4 (the same overlay the GPU ran, 2^24 x 4096: ~30 s on 16
+               threads), a 2^24 sample of C5; this leg is `value`;
       harness  oracle/harness.py, the reference's per-peer Message-List logic
                (sha256 digests in a set per peer, Peer.py:175-216, 395-408) plus
                forwarding, single-core, on BASELINE config 2 (10^4-node BA(m=2),
@@ -165,18 +167,22 @@ def cpu_baseline(args, eng, origin, pkg):
         threads = args.cpu_threads
     churn = args.workload == "c5"
     ncpu = 1 << args.cpu_log2n
-    with pkg.GossipEngine(eng.device) as side:   # the same recipe, device-built (bit-identical to the oracle's)
-        side.build_chung_lu(ncpu, args.dbar, args.gamma, args.seed)
-        g = side.graph()
+    if ncpu == eng.n and eng.nranks == 1:   # the overlay the GPU just ran
+        g = eng.graph()
+    else:
+        with pkg.GossipEngine(eng.device) as side:   # the same recipe, device-built (bit-identical to the oracle's)
+            side.build_chung_lu(ncpu, args.dbar, args.gamma, args.seed)
+            g = side.graph()
     o = pkg.overlay.random_origins(ncpu, args.messages, seed=args.seed)
     t0 = time.perf_counter()
-    ref = oracle_lib.run(g, o, nthreads=threads, want_forwards=False, churn=churn,
+    ref = oracle_lib.run(g, o, nthreads=threads, want_forwards=False, want_seen=False, churn=churn,
                          p_fail=args.p_fail if churn else 0.0, churn_seed=args.seed)
     dt = time.perf_counter() - t0
     sends = sum(s["sends"] for s in ref["stats"])
     out = {"value": sends / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
            "sample": f"oracle/gossip_oracle.c, Chung-Lu gamma={args.gamma} d={args.dbar:g} seed {args.seed} at "
-                     f"2^{args.cpu_log2n} vertices ({g.nnz} arcs), all {len(o)} messages (W = 64), full run"
+                     f"2^{args.cpu_log2n} vertices ({g.nnz} arcs{', the GPU run overlay' if ncpu == eng.n else ''}), "
+                     f"all {len(o)} messages (W = 64), full run"
                      f"{' with churn' if churn else ''} ({ref['rounds']} rounds, {sends} edge-deliveries, "
                      f"{dt:.1f} s, {threads} OpenMP threads)",
            "host": {"nproc": nproc, "affinity": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),

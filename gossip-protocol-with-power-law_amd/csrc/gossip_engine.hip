@@ -183,8 +183,7 @@ struct ExpandArgs {
   int32_t near_done;                   // early-exit round with most messages held: fewer rows in flight
   int32_t pairs;                       // unfiltered W = 64 round: the SCAN_PAIRS variant (late rounds)
   const u64* __restrict__ alive;       // [W] messages some sender forwards this round (or null)
-  const u64* __restrict__ wbits;       // alive rounds after k_want: bit v clear = v holds every alive
-                                       //   message of its component, nothing to scan (or null)
+  int32_t sate;                        // alive early-exit round, no injection left: mark sated receivers
   u64* __restrict__ alive_next;        // [W] the same for round r + 1: OR of the new rows (or null)
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
   const u64* __restrict__ cmk;         // record rounds: dense bitmap of this round's senders (bit v:
@@ -1050,10 +1049,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       L.rp[lane] = b;
       if (lane == 63 || li + 1 == a.nloc) L.rp[lane + 1] = e;
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
-      need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
-      if constexpr (ALIVE) {   // k_want found that v wants no alive message (its 64-vertex word)
-        if (need && a.wbits) need = ((a.wbits[li >> 6] >> lane) & 1ull) != 0ull;
-      }
+      need = !(a.state[v] & (ST_DOWN | ST_SATED)) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
       if constexpr ((MODE & 3) == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
       if constexpr ((MODE & 3) == SCAN_PRE) {
         // sparse filtered rounds: every lane probes the in-list of its own
@@ -1187,6 +1183,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         m &= ~msp;
       }
     }
+    u64 sat = 0;   // receivers of this wave found sated (alive rounds)
     while (m) {
       const int k = __ffsll((long long)m) - 1;
       m &= m - 1;
@@ -1202,6 +1199,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       // (with alive sets a receiver may hold every alive message of its
       // component already: then there is nothing to scan)
       if (ALIVE && ee && a.alive && !__any((want.x | want.y) != 0ull)) {
+        if (a.sate) sat |= 1ull << k;
       } else if constexpr ((MODE & 3) == SCAN_PRE) {
         const uint32_t np = L.np[k];
         if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
@@ -1210,6 +1208,12 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
       }
       reduce_slots<W>(acc);
+      if constexpr (ALIVE) {   // the round's gather covered every alive message v lacked: sated
+        if (a.sate && ee && a.alive) {
+          const u64x2 rem = want & ~acc;
+          if (!__any((rem.x | rem.y) != 0ull)) sat |= 1ull << k;
+        }
+      }
       if constexpr (W == 64 && (MODE & SCAN_CML) != 0) {
         if (a.cmk) {   // the gathered records (gather_scan ORs them into L.racc)
           wave_sync_lds();
@@ -1224,92 +1228,9 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     }
     alive_flush<W>(a, L.alive, lane);
     commit_vertices(a, L, li, need, st);
-  }
-  flush_stats(st, a.partial);
-}
-
-// ---------------------------------------------------------------------------
-// Alive-set pre-check (churn): late early-exit rounds under
-// liveness leave most vertices incomplete for good -- crashes cut some of
-// their component's messages off -- while they already hold every message
-// anyone still forwards (F_r).  The serial loop of k_expand finds that out
-// one receiver at a time (seen row, component mask, then nothing to scan: a
-// dependent chain per vertex, C5 round 6: 62 M of them for 1.3 M receivers).
-// k_want runs the same test, want = cmask & F_r & ~seen, for a wave's 64
-// vertices with Q x RPI rows in flight, and clears the bit of every vertex
-// that wants nothing; k_expand's lane phase then drops those from its serial
-// loop.  Exact: such a vertex would have been skipped there with nothing
-// gathered (acc = 0, no commit).  Vertices this kernel does not check (hubs,
-// no in-arcs, not needy) keep their bit.
-#ifndef GP_WANT_DIV
-#define GP_WANT_DIV 64.0   // pre-check when last round's new bits <= n*m / GP_WANT_DIV (0: never)
-#endif
-// (the environment variable GP_WANT_DIV overrides it: the parity suite runs
-// the alive rounds with the pre-check forced on and off)
-static double want_div() {
-  const char* e = getenv("GP_WANT_DIV");
-  return e && *e ? atof(e) : GP_WANT_DIV;
-}
-template <int W>
-__global__ __launch_bounds__(BLOCK) void k_want(ExpandArgs a, u64* __restrict__ wbits) {
-  constexpr int LPR = Geo<W>::LPR;
-  constexpr int RPI = Geo<W>::RPI;
-  constexpr int Q = 4;   // row wave-instructions in flight (seen + mask pieces each)
-  const int lane = threadIdx.x & 63;
-  const int wib = uniform(threadIdx.x >> 6);
-  const int g = lane / LPR, lw = lane % LPR;
-  WaveStats st;
-  ws_zero(st);
-  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
-  if (base < a.nloc) {
-    const int64_t li = base + lane;
-    bool need = false;
-    uint32_t slot = SLOT_NONE;
-    int32_t mrow = 0;
-    if (li < a.nloc) {
-      const int v = (int)(a.vbegin + li);
-      const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
-      need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && e - b <= a.hub_thr && e > b;
-      if (need) {
-        slot = a.sp[v];
-        mrow = a.midx[v];
-      }
+    if constexpr (ALIVE) {
+      if (sat && ((sat >> lane) & 1ull)) const_cast<uint8_t*>(a.state)[a.vbegin + li] |= ST_SATED;
     }
-    u64 m = __ballot(need);
-    const u64x2 fa = load_piece<W>(a.alive, 0, lw);
-    u64 drop = 0;        // this lane's share of the wave's "wants nothing" bits
-    uint32_t nseen = 0;  // seen rows read (lw == 0 lanes count their vertex)
-    while (m) {
-      const int cnt = __popcll(m);
-      int kk[Q];
-      u64x2 sv[Q], cm[Q];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int t = q * RPI + g;
-        kk[q] = t < cnt ? select_bit(m, t + 1) : -1;
-        const int kq = kk[q] >= 0 ? kk[q] : 0;
-        const uint32_t s = (uint32_t)__shfl((int)slot, kq);
-        const int32_t mr = __shfl(mrow, kq);
-        sv[q] = u64x2{0, 0};
-        cm[q] = u64x2{0, 0};
-        if (kk[q] >= 0) {
-          if (s != SLOT_NONE) sv[q] = load_piece<W>(a.slot[s], a.vbegin + base + kq, lw);
-          cm[q] = load_piece<W>(a.cmask, mr, lw);
-          if (lw == 0 && s != SLOT_NONE) ++nseen;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const u64x2 w = cm[q] & fa & ~sv[q];
-        const bool any = group_or<LPR>((w.x | w.y) != 0ull);
-        if (kk[q] >= 0 && !any && lw == 0) drop |= 1ull << kk[q];
-      }
-      for (int i = 0; i < Q * RPI && m; ++i) m &= m - 1;   // the vertices just checked
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) drop |= __shfl_xor(drop, o);
-    st.add(S_SEEN_READ, (u64)wave_sum_u32(nseen));
-    if (lane == 0) wbits[base >> 6] = ~drop;
   }
   flush_stats(st, a.partial);
 }
@@ -1524,7 +1445,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
         if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
         const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
         const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
-        need = !(a.state[v] & ST_DOWN) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
+        need = !(a.state[v] & (ST_DOWN | ST_SATED)) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
         if (!need && !hub) a.fpop_next[v] = 0;
       }
       st.add(S_SENDS, wave_sum_u64(sends));
@@ -1959,7 +1880,8 @@ __global__ __launch_bounds__(BLOCK) void k_mkneed(const uint8_t* __restrict__ st
   for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
     const int64_t v = v0 + lane;
     bool ok = false;
-    if (v >= vbegin && v < vbegin + nloc) ok = !(state[v] & ST_DOWN) && seenpop[v - vbegin] < done_at[v];
+    if (v >= vbegin && v < vbegin + nloc)
+      ok = !(state[v] & (ST_DOWN | ST_SATED)) && seenpop[v - vbegin] < done_at[v];
     const u64 m = __ballot(ok);
     if (lane == 0) nbits[v0 >> 6] = m;
   }
@@ -1990,9 +1912,9 @@ __global__ __launch_bounds__(BLOCK) void k_apply_lanes(ExpandArgs a) {
   WaveStats st;
   ws_zero(st);
   const int64_t nt = (int64_t)a.stats[S_TOUCH_CURSOR];
-  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
-  if (base < nt) {
-    alive_zero<W>(a, L.alive, lane);
+  alive_zero<W>(a, L.alive, lane);
+  const int64_t stride = (int64_t)gridDim.x * WAVES * 64;
+  for (int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64; base < nt; base += stride) {
     const bool mine = base + lane < nt;
     const int v = mine ? a.touched[base + lane] : 0;
     const uint32_t slot_of = mine ? (uint32_t)a.sp[v] : SLOT_NONE;
@@ -2057,8 +1979,9 @@ __global__ __launch_bounds__(BLOCK) void k_apply_lanes(ExpandArgs a) {
     st.add(S_WRITTEN, wave_sum_u64(nrecv));
     st.add(S_NEXT_ARCS, wave_sum_u64(narcs));
     st.add(S_SEEN_READ, wave_sum_u64(nseen));
-    alive_flush<W>(a, L.alive, lane);
+    wave_sync_lds();   // L.tot / L.dig are restaged by the next group
   }
+  alive_flush<W>(a, L.alive, lane);
   flush_stats(st, a.partial);
 }
 
@@ -3017,7 +2940,9 @@ static void launch_push_w(Ctx* c, ExpandArgs a) {
   hipStream_t s = c->stream;
   const int64_t nwords = (c->n_alloc + 63) / 64;
   constexpr bool lanes = W <= GP_PUSH_LANES_MAXW;
-  if (lanes) {
+  // the bitmap pays once the push has many arcs (a pass over n vertices
+  // against three scattered loads per arc)
+  if (lanes && c->push_est * 16.0 >= (double)c->n_alloc) {
     hipLaunchKernelGGL(k_mkneed, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
                        dim3(BLOCK), 0, s, c->d_state, c->d_seenpop, c->d_done_at, a.vbegin, a.nloc, c->n_alloc,
                        c->d_nbits);
@@ -3029,8 +2954,10 @@ static void launch_push_w(Ctx* c, ExpandArgs a) {
   hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_touch_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_tbits, nwords,
                      c->d_touched, c->d_stats);
-  if (lanes)   // one wave per 64 touched receivers; the grid covers every vertex
-    hipLaunchKernelGGL(k_apply_lanes<W>, dim3(grid_for(std::max<int64_t>(c->nloc(), 1), (int64_t)WAVES * 64)),
+  if (lanes)   // a wave per 64 touched receivers at a time, grid-stride
+    hipLaunchKernelGGL(k_apply_lanes<W>, dim3(std::max(1, std::min(grid_for(std::max<int64_t>(c->nloc(), 1),
+                                                                             (int64_t)WAVES * 64),
+                                                                    c->cu_count * 8))),
                        dim3(BLOCK), 0, s, a);
   else
     hipLaunchKernelGGL(k_apply<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
@@ -3072,16 +2999,6 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   }
   const int mode = a.unfiltered ? SCAN_UNFILTERED : SCAN_FILTERED;
   (void)hipEventRecord(c->ev[4], c->stream);
-  // alive-set pre-check (k_want) ahead of the per-receiver kernel's alive variants
-  if constexpr (W >= 32) {
-    if (a.wbits && !flat && a.alive && a.early_exit && a.nloc > 0)
-      hipLaunchKernelGGL(k_want<W>, dim3(grid_for(a.nloc, per_block)), dim3(BLOCK), 0, c->stream, a,
-                         const_cast<u64*>(a.wbits));
-    else
-      a.wbits = nullptr;
-  } else {
-    a.wbits = nullptr;
-  }
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
     const dim3 grid(grid_for(a.nloc, (int64_t)WAVES * FlatNR<W>::value));
     if constexpr (W <= 32) {
@@ -3181,10 +3098,15 @@ static int launch_expand(Ctx* c) {
   // narrow rows push at a lower ratio: the pull's per-arc scan does not
   // shrink with W, the push's row words do (k_apply_lanes, k_mkneed)
 #ifndef GP_NARROW_PUSH_SCALE
-#define GP_NARROW_PUSH_SCALE 1.0
+#define GP_NARROW_PUSH_SCALE 0.25
 #endif
-  const double ratio = c->cfg.push_ratio * (c->words <= 16 ? GP_NARROW_PUSH_SCALE : 1.0);
+  // (early rounds only: late rounds' pulls skip the done receivers, which the
+  // estimate does not see -- the 512-message shard's round 6 pulls in 0.27 ms
+  // and pushes in 0.72)
+  const bool early = (double)c->held_bits * 2.0 < (double)c->n * (double)c->m;
+  const double ratio = c->cfg.push_ratio * (c->words <= 16 && early ? GP_NARROW_PUSH_SCALE : 1.0);
   c->mode_push = c->cfg.push_ratio > 0.0 && est * ratio <= (double)c->nnz;
+  c->push_est = est;
   if (c->mode_push && c->nloc() > 0)
     GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1], 0, (size_t)c->nloc() * 4, c->stream));
   // unfiltered pull when (nearly) every vertex is a sender: last round's
@@ -3254,16 +3176,12 @@ static int launch_expand(Ctx* c) {
 #endif
   a.pairs = GP_PAIRS_DIV > 0.0 && a.near_done && a.unfiltered &&
             (double)c->prev_new_bits * GP_PAIRS_DIV <= (double)c->n * (double)c->m ? 1 : 0;
-  // alive-set pre-check (k_want): early-exit rounds under liveness once the
-  // rounds have gone sparse (most incomplete vertices already hold every
-  // message still forwarded)
-  a.wbits = nullptr;
-  const double wdiv = want_div();
-  if (wdiv > 0.0 && alive_on(c) && c->early_exit_now && !c->mode_push && c->words >= 32 &&
-      (double)c->prev_new_bits * wdiv <= (double)c->n * (double)c->m) {
-    if (!c->d_wbits) GP_TRY(dalloc(&c->d_wbits, (size_t)(c->n_alloc + 63) / 64 + 1));
-    a.wbits = c->d_wbits;
-  }
+  // sated vertices (churn): with no injection left, a receiver that ends the
+  // round holding every alive message of its component never receives again
+#ifndef GP_SATE
+#define GP_SATE 1
+#endif
+  a.sate = GP_SATE && alive_on(c) && c->early_exit_now && c->round >= c->last_inject_round ? 1 : 0;
   switch (c->words) {
     case 1: launch_expand_w<1>(c, a); break;
     case 2: launch_expand_w<2>(c, a); break;
@@ -3378,7 +3296,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
-  dfree(&c->d_midx); dfree(&c->d_cmask); dfree(&c->d_wbits);
+  dfree(&c->d_midx); dfree(&c->d_cmask);
   bitcount_free(c);
   c->d_msg_fwd = nullptr;
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
@@ -3670,7 +3588,7 @@ void gp_destroy(gp_ctx* c) {
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
   dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
-  dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask); dfree(&c->d_wbits);
+  dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
   dfree(&c->d_slot[2]);
@@ -4320,8 +4238,8 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(n));
       GP_TRY(copy_sync(c, host, what == GP_STATE ? c->d_state : c->d_miss, (size_t)n, hipMemcpyDeviceToHost));
-      if (what == GP_STATE)   // (the per-round removal flag is exchange bookkeeping)
-        for (int64_t v = 0; v < n; ++v) static_cast<uint8_t*>(host)[v] &= (uint8_t)~ST_RMNEW;
+      if (what == GP_STATE)   // (the removal flag and the sated mark are engine bookkeeping)
+        for (int64_t v = 0; v < n; ++v) static_cast<uint8_t*>(host)[v] &= (uint8_t)~(ST_RMNEW | ST_SATED);
       return 0;
     case GP_DEG_LIVE:
       if (!run) return set_error(GP_ESTATE, "no run state");

@@ -138,8 +138,8 @@ struct Ctx {
   uint32_t* d_det_cur = nullptr;
   u64* d_det_base = nullptr;
   // [n_alloc/64] frontier_r activity bitmap (fpop != 0): 2 MB at 2^24
+  double push_est = 0.0;            // sender arcs the direction estimate saw this round
   u64* d_nbits = nullptr;           // [n_alloc/64] narrow push rounds: receivable vertices (k_mkneed)
-  u64* d_wbits = nullptr;           // [n_alloc/64] k_want: bit v clear = wants no alive message this round
   u64* d_abits = nullptr;
   u64* d_sbits = nullptr;   // summary level of d_abits (GP_SUMMARY_PROBE builds)
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
@@ -285,6 +285,10 @@ int exchange_group(Ctx** ctxs, int32_t nctx);  // the same through device-to-dev
 // state bit: removed by this rank's seed step in the current round (sent to the
 // ranks holding the vertex as a ghost; cleared by the next round's k_churn)
 constexpr uint8_t ST_RMNEW = 8;
+// sated (churn runs): no injection left and v holds every
+// message of its component that anyone still forwards; the alive sets only
+// shrink from round to round, so v never receives again and the pull skips it
+constexpr uint8_t ST_SATED = 16;
 
 }  // namespace gp
 

@@ -101,8 +101,9 @@ def digest_from_first(first, origin, word_base=0):
 
 def run(csr, origin, inject_round=None, churn=False, p_fail=0.0, churn_seed=0, miss_threshold=3,
         crashes=(), max_rounds=254, nthreads=1, want_first=False, want_forwards=True,
-        report_cap=1 << 20):
-    """Full propagation on the CPU.  crashes: iterable of (vertex, round)."""
+        report_cap=1 << 20, want_seen=True):
+    """Full propagation on the CPU.  crashes: iterable of (vertex, round).
+    want_seen=False skips the Message-List copy-out (8 GiB at C4)."""
     lib = load()
     n = int(csr.n)
     origin = np.ascontiguousarray(origin, dtype=np.int32)
@@ -119,7 +120,7 @@ def run(csr, origin, inject_round=None, churn=False, p_fail=0.0, churn_seed=0, m
     cr = np.array(list(crashes), dtype=np.int32).reshape(-1, 2)
     cv = np.ascontiguousarray(cr[:, 0])
     crd = np.ascontiguousarray(cr[:, 1])
-    seen = np.zeros((n, W), np.uint64)
+    seen = np.zeros((n, W), np.uint64) if want_seen else None
     first = np.zeros((n, m), np.uint8) if want_first else None
     digest = np.zeros(n, np.uint64)
     cov = np.zeros(m, np.uint64)

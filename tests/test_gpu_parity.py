@@ -509,21 +509,21 @@ def test_wide_rows_churn(pkg, oracle, mode):
     r["eng"].close()
 
 
-@pytest.mark.parametrize("want_div", ["0", "1e30"], ids=["precheck-off", "precheck-always"])
+@pytest.mark.parametrize("schedule", ["round0", "spread"])
 @pytest.mark.parametrize("m", [4096, 2048])
 @pytest.mark.parametrize("mode", [MODES[0], MODES[2], MODES[4]], ids=["pull", "pull-unfiltered", "adaptive"])
-def test_alive_precheck(pkg, oracle, monkeypatch, want_div, m, mode):
-    """k_want: in early-exit rounds under churn, vertices
-    that already hold every alive message of their component are dropped
-    before the per-receiver loop.  Forced on in every such round, and off,
-    the outputs equal the oracle's (Peer.py:298-313 liveness, Seed.py:358-406
-    removal, forward-once)."""
-    monkeypatch.setenv("GP_WANT_DIV", want_div)
+def test_sated_vertices(pkg, oracle, schedule, m, mode):
+    """Sated vertices: under churn, once no injection is
+    left, a receiver that ends an early-exit round holding every alive message
+    of its component is skipped by every later pull (the alive sets only
+    shrink).  All injections at round 0 (sated from the first early-exit
+    round on) or spread over rounds 0-2; outputs equal the oracle's
+    (Peer.py:298-313 liveness, Seed.py:358-406 removal, forward-once)."""
     push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     rp, col = oracle.chung_lu(40_000, 12, 2.4, 31)
     g = pkg.CSR(40_000, rp, col, False)
     origin = pkg.overlay.random_origins(g.n, m, seed=31)
-    inject = (np.arange(m) % 3).astype(np.int32)
+    inject = np.zeros(m, np.int32) if schedule == "round0" else (np.arange(m) % 3).astype(np.int32)
     r = _compare(pkg, oracle, g, origin, inject, first=False, hub_threshold=256, push_ratio=push_ratio,
                  unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask,
                  churn=True, p_fail=0.02, churn_seed=7)
