@@ -1593,6 +1593,209 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
   flush_stats(st, a.partial);
 }
 
+// ---------------------------------------------------------------------------
+// Record pull (W = 64, compact Message-Lists read, no early exit: C4's round
+// 2 with compact_rows).  The per-receiver loop of k_expand gathers records one
+// receiver at a time, a chain of dependent round trips per receiver that the
+// 128-B records cannot amortise (round 2: row bytes halve, time does not
+// move).  Here a wave streams the in-arcs of REC_NR receivers as one flat
+// sequence: column ids and probes of 64 arcs at a time, then the active
+// sparse senders' records 8 per wave-instruction (8 lanes x 16 B, REC_RIF
+// instructions in flight) and the dense senders' full rows 2 per
+// instruction, every word OR-ed into its receiver's 512-B accumulator in LDS
+// (ds_or_b64; a record's word p >= 1 goes to word select_bit(mask, p)).  The
+// receiver side runs two receivers per instruction through pair_finish
+// (rows, records of the next round, first bytes, digest).
+constexpr int REC_NR = 8;
+#ifndef GP_REC_RIF
+#define GP_REC_RIF 4
+#endif
+#ifndef GP_REC_FLAT
+#define GP_REC_FLAT 1
+#endif
+struct RecLds {
+  static constexpr bool kPre = false, kCml = true;
+  u64 acc[REC_NR][64];   // OR accumulators of the wave's receivers
+  int32_t sid[64];       // active sparse senders of one chunk (records)
+  int32_t did[64];       // active dense senders of one chunk (full rows)
+  int8_t sown[64];       // their receiver
+  int8_t down[64];
+  uint32_t tot[REC_NR];  // pair_finish: new bits of receiver k
+  u64 dig[REC_NR];       // its digest terms
+  uint8_t cd[REC_NR];    // its new row is dense (no record)
+  u64 alive[64];         // alive_add (unused: record rounds run without liveness alive sets too)
+};
+
+__global__ __launch_bounds__(BLOCK) void k_expand_rec(ExpandArgs a) {
+  constexpr int W = 64;
+  __shared__ RecLds s_r[WAVES];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  RecLds& L = s_r[wib];
+  WaveStats st;
+  ws_zero(st);
+  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * REC_NR;
+  if (base < a.nloc) {
+    const int64_t li = base + lane;
+    const bool mine = lane < REC_NR && li < a.nloc;
+    const int v = mine ? (int)(a.vbegin + li) : 0;
+    bool need = false, act = false;
+    u64 sends = 0;
+    int64_t b = 0;
+    uint32_t deg = 0;
+    if (mine) {
+      const uint32_t fp = a.fpop[v];
+      act = fp != 0u;
+      if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
+      b = a.row_ptr[v];
+      const int64_t e = a.row_ptr[v + 1];
+      const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
+      need = !(a.state[v] & (ST_DOWN | ST_SATED)) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
+      if (!need && !hub) a.fpop_next[v] = 0;
+      if (need) deg = (uint32_t)(e - b);
+    }
+    st.add(S_SENDS, wave_sum_u64(sends));
+    st.add(S_ACTIVE, (u64)__popcll(__ballot(act)));
+    const u64 needm = __ballot(need);
+    st.add(S_VISITED, (u64)__popcll(needm));
+    if (lane < REC_NR) {
+      L.tot[lane] = 0u;
+      L.dig[lane] = 0ull;
+      L.cd[lane] = 1;
+    }
+    alive_zero<W>(a, L.alive, lane);
+    u64 gathered = 0, rbytes = 0;
+    if (needm) {
+#pragma unroll
+      for (int q = 0; q < REC_NR; ++q) L.acc[q][lane] = 0ull;
+      wave_sync_lds();
+      const uint32_t excl = wave_excl_scan_u32(deg, lane);
+      const uint32_t T = (uint32_t)__shfl((int)(excl + deg), 63);
+      const uint32_t blo = (uint32_t)b, bhi = (uint32_t)((u64)b >> 32);
+      st.add(S_ARCS, T);
+      const int gq = lane >> 3, sl = lane & 7;     // record lanes: 8 records per instruction
+      const int h = lane >> 5, lw = lane & 31;     // row lanes: 2 rows per instruction
+      for (uint32_t c0 = 0; c0 < T; c0 += 64) {
+        const uint32_t p = c0 + (uint32_t)lane;
+        int own = -1;
+#pragma unroll
+        for (int r = 0; r < REC_NR; ++r) {
+          const uint32_t er = (uint32_t)__shfl((int)excl, r), dr = (uint32_t)__shfl((int)deg, r);
+          if (dr && p >= er && p < er + dr) own = r;
+        }
+        const int src = own >= 0 ? own : 0;
+        const int64_t bo = (int64_t)(((u64)(uint32_t)__shfl((int)bhi, src) << 32) | (u64)(uint32_t)__shfl((int)blo, src));
+        const uint32_t eo = (uint32_t)__shfl((int)excl, src);
+        int32_t u = -1;
+        bool dense = false;
+        if (p < T && own >= 0) {
+          u = a.gcol[bo + (int64_t)(p - eo)];
+          if (((a.abits[u >> 6] >> (u & 63)) & 1ull) == 0ull) u = -1;
+          else dense = ((a.cmk[u >> 6] >> (u & 63)) & 1ull) != 0ull;
+        }
+        const u64 ms = __ballot(u >= 0 && !dense), md = __ballot(u >= 0 && dense);
+        if (u >= 0) {
+          if (dense) {
+            L.did[lane_rank(md)] = u;
+            L.down[lane_rank(md)] = (int8_t)own;
+          } else {
+            L.sid[lane_rank(ms)] = u;
+            L.sown[lane_rank(ms)] = (int8_t)own;
+          }
+        }
+        wave_sync_lds();
+        const int ns = __popcll(ms), nd = __popcll(md);
+        gathered += (u64)(ns + nd);
+        rbytes += (u64)ns * (8 * CML_WORDS) + (u64)nd * (8 * W);
+        for (int k0 = 0; k0 < ns; k0 += 8 * GP_REC_RIF) {
+          u64x2 rv[GP_REC_RIF];
+#pragma unroll
+          for (int t = 0; t < GP_REC_RIF; ++t) {
+            const int k = k0 + t * 8 + gq;
+            rv[t] = u64x2{0, 0};
+            if (k < ns) rv[t] = *reinterpret_cast<const u64x2*>(a.cml + (size_t)L.sid[k] * CML_WORDS + 2 * sl);
+          }
+#pragma unroll
+          for (int t = 0; t < GP_REC_RIF; ++t) {
+            const int k = k0 + t * 8 + gq;
+            const u64 mask = __shfl(rv[t].x, lane & ~7);   // word 0 of the record: its word mask
+            if (k < ns) {
+              const int c = __popcll(mask);
+              u64* acc = L.acc[L.sown[k]];
+              if (sl > 0 && 2 * sl <= c && rv[t].x) atomicOr(&acc[select_bit(mask, 2 * sl)], rv[t].x);
+              if (2 * sl + 1 <= c && rv[t].y) atomicOr(&acc[select_bit(mask, 2 * sl + 1)], rv[t].y);
+            }
+          }
+        }
+        for (int k0 = 0; k0 < nd; k0 += 4) {
+          u64x2 r0 = u64x2{0, 0}, r1 = u64x2{0, 0};
+          const int ka = k0 + h, kb = k0 + 2 + h;
+          if (ka < nd) r0 = load_piece<W>(a.rows, L.did[ka], lw);
+          if (kb < nd) r1 = load_piece<W>(a.rows, L.did[kb], lw);
+          if (ka < nd) {
+            u64* acc = L.acc[L.down[ka]];
+            if (r0.x) atomicOr(&acc[2 * lw], r0.x);
+            if (r0.y) atomicOr(&acc[2 * lw + 1], r0.y);
+          }
+          if (kb < nd) {
+            u64* acc = L.acc[L.down[kb]];
+            if (r1.x) atomicOr(&acc[2 * lw], r1.x);
+            if (r1.y) atomicOr(&acc[2 * lw + 1], r1.y);
+          }
+        }
+        wave_sync_lds();
+      }
+    }
+    st.add(S_GATHERED, gathered);
+    st.add(S_ROW_BYTES, rbytes);
+    // receiver side: two receivers per instruction, a half-wave per row
+    const int h = lane >> 5, lw = lane & 31;
+    const uint32_t slot_of = need ? (uint32_t)a.sp[v] : SLOT_NONE;
+    wave_sync_lds();
+    if (needm) {
+      for (int k0 = 0; k0 < REC_NR; k0 += 2) {
+        const int ks = k0 + h;
+        const bool on = ((needm >> ks) & 1ull) != 0ull;
+        const int vs = __shfl(v, ks);
+        const uint32_t sslot = (uint32_t)__shfl((int)slot_of, ks);
+        u64x2 acc = u64x2{0, 0};
+        if (on) {
+          acc.x = L.acc[ks][2 * lw];
+          acc.y = L.acc[ks][2 * lw + 1];
+        }
+        const u64x2 sv = pair_seen<W>(a, h, lw, on, k0 + 1, vs, sslot, acc, st);
+        pair_finish<W>(a, L, h, lw, on, ks, k0 + 1, base + ks, vs, acc, sv, st);
+      }
+    }
+    wave_sync_lds();
+    u64 next_arcs = 0;
+    if (need) {
+      const uint32_t tot = L.tot[lane];
+      a.fpop_next[v] = tot;
+      if (tot) {
+        a.seenpop[li] += tot;
+        a.sp[v] = (uint8_t)a.wslot;
+        a.ws[v] |= (uint8_t)(1u << a.wslot);
+        if (a.digest) a.digest[li] ^= L.dig[lane];
+        next_arcs = (u64)(uint32_t)max(a.deg_live[v], 0);
+      }
+    }
+    st.add(S_NEXT_ARCS, wave_sum_u64(next_arcs));
+    if (a.cmk_next) {   // this wave's bits of the next round's dense bitmap (1: read the full row)
+      const u64 dm = __ballot(mine && (!need || L.tot[lane] == 0u || L.cd[lane] != 0));
+      const u64 mm = __ballot(mine);
+      if (lane == 0) {
+        const int sh = (int)(base & 63);
+        u64* wd = a.cmk_next + (base >> 6);
+        if (dm) atomicOr(wd, dm << sh);
+        if (mm & ~dm) atomicAnd(wd, ~((mm & ~dm) << sh));
+      }
+    }
+    alive_flush<W>(a, L.alive, lane);
+  }
+  flush_stats(st, a.partial);
+}
+
 // hubs, pass 1: one wave per (hub, arc chunk) -> partial OR row
 template <int W, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
@@ -1608,7 +1811,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
     const HubItem h = a.hub_items[it];
     const int64_t i = h.v - a.vbegin;
     u64x2 acc = {0, 0};
-    if (!(a.state[h.v] & ST_DOWN) && a.seenpop[i] < a.done_at[h.v]) {
+    if (!(a.state[h.v] & (ST_DOWN | ST_SATED)) && a.seenpop[i] < a.done_at[h.v]) {
       const bool ee = a.early_exit != 0;
       u64x2 want = {0, 0};
       if (ee) want = early_exit_target<W>(a, h.v, s_w[wib], g, lw, a.sp[h.v], a.midx[h.v]);
@@ -1638,7 +1841,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
   if (h < a.n_items) {
     const int v = a.hubs[h];
     const int64_t i = v - a.vbegin;
-    if ((a.state[v] & ST_DOWN) || a.seenpop[i] >= a.done_at[v]) {
+    if ((a.state[v] & (ST_DOWN | ST_SATED)) || a.seenpop[i] >= a.done_at[v]) {
       if (lane == 0) a.fpop_next[v] = 0;
     } else {
       st.add(S_VISITED, 1);
@@ -1717,7 +1920,7 @@ __device__ __forceinline__ void push_arcs(const ExpandArgs& a, int64_t jb, int64
       const int q = (int)(t - j * nnz);
       v = a.ocol[jb + j];
       const bool recv = a.nbits ? ((a.nbits[v >> 6] >> (v & 63)) & 1ull) != 0ull
-                                : (v >= a.vbegin && v < a.vbegin + a.nloc && !(a.state[v] & ST_DOWN) &&
+                                : (v >= a.vbegin && v < a.vbegin + a.nloc && !(a.state[v] & (ST_DOWN | ST_SATED)) &&
                                    a.seenpop[v - a.vbegin] < a.done_at[v]);
       if (recv) {
         const int w = swords[q];
@@ -3030,7 +3233,10 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
       hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(BLOCK), 0, c->stream, a);
     else if (W == 64 && (a.cmk || a.cmk_next)) {   // compact Message-Lists read and / or written
       if constexpr (W == 64) {
-        if (c->prefilter_now)
+        if (GP_REC_FLAT && a.cmk && !a.early_exit && !c->prefilter_now && !a.alive)
+          hipLaunchKernelGGL(k_expand_rec, dim3(grid_for(a.nloc, (int64_t)WAVES * REC_NR)), dim3(BLOCK), 0,
+                             c->stream, a);
+        else if (c->prefilter_now)
           hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_CML>), grid, dim3(BLOCK), 0, c->stream, a);
         else
           hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_CML>), grid, dim3(BLOCK), 0, c->stream, a);
