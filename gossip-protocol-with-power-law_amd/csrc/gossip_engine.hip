@@ -3191,7 +3191,15 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 #endif
   const bool flat_nd = GP_FLAT_NEAR_DONE && W == 32 && c->cfg.flat_max_words > 0 && a.near_done &&
                        (double)c->prev_new_bits * 4.0 >= (double)c->n * (double)c->m;
-  const bool flat = W <= 32 && (W <= c->cfg.flat_max_words || flat_nd);
+  // W = 32 in a dense filtered round without early exit (a shard's round 2):
+  // the flat kernel's arc stream beats the per-receiver loop there (10.3 ->
+  // 9.8 ms on the 2048-message shard)
+#ifndef GP_FLAT_DENSE32
+#define GP_FLAT_DENSE32 0
+#endif
+  const bool flat_d32 = GP_FLAT_DENSE32 && W == 32 && c->cfg.flat_max_words > 0 && !a.unfiltered &&
+                        !a.early_exit && !c->prefilter_now && !c->arc_mask_now;
+  const bool flat = W <= 32 && (W <= c->cfg.flat_max_words || flat_nd || flat_d32);
   const bool masked = !a.unfiltered && !flat && c->arc_mask_now;
   if (masked) {   // mask words of the owned vertices' in-arcs
     const int64_t kb = c->h_row_ptr[0] >> 6;
@@ -3310,7 +3318,10 @@ static int launch_expand(Ctx* c) {
   // estimate does not see -- the 512-message shard's round 6 pulls in 0.27 ms
   // and pushes in 0.72)
   const bool early = (double)c->held_bits * 2.0 < (double)c->n * (double)c->m;
-  const double ratio = c->cfg.push_ratio * (c->words <= 16 && early ? GP_NARROW_PUSH_SCALE : 1.0);
+#ifndef GP_NARROW_PUSH_MAXW
+#define GP_NARROW_PUSH_MAXW 16
+#endif
+  const double ratio = c->cfg.push_ratio * (c->words <= GP_NARROW_PUSH_MAXW && early ? GP_NARROW_PUSH_SCALE : 1.0);
   c->mode_push = c->cfg.push_ratio > 0.0 && est * ratio <= (double)c->nnz;
   c->push_est = est;
   if (c->mode_push && c->nloc() > 0)
