@@ -194,7 +194,7 @@ def _full_size(pkg, oracle, log2n, seed, churn):
     assert np.array_equal(dig, w_dig)
     assert np.array_equal(np.concatenate([p["cov"] for p in parts]), w_cov)
     assert np.array_equal(np.concatenate([p["fwd"] for p in parts]), w_fwd)
-    return dict(stats=w_stats, cov=w_cov, fwd=w_fwd, g=g, origin=origin, cfg=cfg, fps=w_fps)
+    return dict(stats=w_stats, cov=w_cov, fwd=w_fwd, dig=w_dig, g=g, origin=origin, cfg=cfg, fps=w_fps)
 
 
 @pytest.mark.timeout(900)
@@ -203,6 +203,20 @@ def test_c4_full_size_parity(pkg, oracle):
     whole W = 64 run against the oracle's run of all 4096 messages."""
     out = _full_size(pkg, oracle, 24, 4, churn=False)
     assert out["stats"][-1]["new_bits"] == 0
+    # the same run with compact Message-Lists (round 2 through the flat record
+    # pull, k_expand_rec): identical to the oracle-checked run
+    with pkg.GossipEngine(0, compact_rows=1, **out["cfg"]) as eng:
+        eng.load_graph(out["g"])
+        eng.set_messages(out["origin"])
+        eng.reset()
+        stats, _ = _run(eng)
+        assert any(s["scan"] & 4 for s in stats)
+        for a, b in zip(stats, out["stats"]):
+            for k in STAT_KEYS:
+                assert a[k] == b[k], (k, a["round"])
+        assert np.array_equal(eng.coverage(), out["cov"])
+        assert np.array_equal(eng.forwards(), out["fwd"])
+        assert np.array_equal(eng.digest(), out["dig"])
 
 
 @pytest.mark.timeout(1200)

@@ -346,6 +346,41 @@ def test_group_partition_invariance(pkg, oracle, mode, churn, by_arcs):
             e.close()
 
 
+@pytest.mark.parametrize("churn", [False, True])
+def test_group_partition_at_scale(pkg, oracle, churn):
+    """Vertex partition at 2^20 vertices (Chung-Lu, 16.7 M arcs) x 512
+    messages over P = 4 arc-balanced slices: per-round counters, digests,
+    Message-Lists, coverage and forwards equal the one-context run's, which
+    the oracle pins (run here too at this size)."""
+    n = 1 << 20
+    rp, col = oracle.chung_lu(n, 16, 2.5, 12)
+    g = pkg.CSR(n, rp, col, False)
+    origin = pkg.overlay.random_origins(n, 512, seed=12)
+    cfg = dict(track_msg_forwards=int(churn), partition_by_arcs=1)
+    kw = {}
+    if churn:
+        cfg.update(churn=1, p_fail=0.01, churn_seed=4)
+        kw = dict(churn=True, p_fail=0.01, churn_seed=4)
+    engs, stats, _ = _group_run(pkg, g, origin, None, 4, **cfg)
+    ref = oracle.run(g, origin, nthreads=int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1),
+                     report_cap=1 << 24, **kw)
+    assert len(stats) == ref["rounds"]
+    for a, b in zip(stats, ref["stats"]):
+        for k in STAT_KEYS:
+            assert a[k] == b[k], (k, a["round"], a[k], b[k])
+    assert sum(s["xchg_rows"] for s in stats) > 0
+    assert np.array_equal(np.concatenate([e.digest() for e in engs]), ref["digest"])
+    assert np.array_equal(np.concatenate([e.seen() for e in engs]), ref["seen"])
+    cov = fwd = 0
+    for e in engs:
+        e.finalize()
+        cov = cov + e.coverage()
+        fwd = fwd + e.forwards()
+        e.close()
+    assert np.array_equal(cov, ref["coverage"])
+    assert np.array_equal(fwd, ref["forwards"])
+
+
 @pytest.mark.parametrize("by_arcs", [0, 1], ids=["vertex-slices", "arc-slices"])
 def test_partition_local_graph(pkg, by_arcs):
     """The local CSR of a partition: owned rows are the global in-lists
@@ -656,11 +691,11 @@ def test_wide_rows_no_churn(pkg, oracle, mode):
 @pytest.mark.parametrize("churn", [False, True])
 def test_compact_message_lists(pkg, oracle, prefilter, churn):
     """W = 64, every message injected at round 0 on a sparse overlay: the early
-    rounds gather senders from compact Message-Lists (scan bit 4; receivers of
-    up to GP_QUAD_DEG in-arcs four at a time in rec_quads, the rest one at a
-    time), with and without the lane-parallel prefilter, with churn (exact
-    frontier rows, alive sets); results are those of the oracle (first-receipt
-    matrix included) and of a run with compact rows off."""
+    rounds gather senders from compact Message-Lists (scan bit 4): without the
+    prefilter through the flat record pull (k_expand_rec, 8 receivers per wave,
+    4 record instructions in flight), with it through the per-receiver loop;
+    with churn (exact frontier rows, alive sets); results are those of the
+    oracle (first-receipt matrix included) and of a run with compact rows off."""
     rp, col = oracle.chung_lu(200_000, 8, 2.5, 31)
     g = pkg.CSR(200_000, rp, col, False)
     origin = pkg.overlay.random_origins(g.n, 4096, seed=31)
