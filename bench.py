@@ -283,7 +283,7 @@ def main():
         for s in runs[-1]:
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
-                                                "rows_written", "row_bytes", "atomics",
+                                                "rows_written", "row_bytes", "atomics", "done_nb",
                                                 "crashed", "reports", "removals", "scan", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None

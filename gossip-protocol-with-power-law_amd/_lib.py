@@ -56,6 +56,7 @@ class RoundStats(ctypes.Structure):
         ("kernel_ms", ctypes.c_double),
         ("xchg_rows", ctypes.c_uint64),
         ("xchg_bytes", ctypes.c_uint64),
+        ("done_nb", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -126,7 +127,7 @@ SIGNATURES = {
     "gp_checkpoint_load": (ctypes.c_int, [_P, _P, _I64]),
 }
 
-ABI_VERSION = 13   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 14   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

@@ -175,6 +175,8 @@ struct ExpandArgs {
   const uint32_t* __restrict__ fpop;   // |frontier_r|: bits received in round r - 1 (+ injected)
   const u64* __restrict__ abits;       // bit v: fpop(v) != 0 (2 MB at 2^24)
   const u64* __restrict__ sbits;       // bit k: abits[k] != 0 (sparse probe rounds of big overlays; else null)
+  const u64* __restrict__ dbits;       // early-exit rounds without liveness: bit u = u held every message
+                                       //   of its component at the end of the last round (else null)
   const int32_t* __restrict__ gcol;    // in-CSR columns in gather order (neighbour degree desc)
   const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
@@ -986,6 +988,68 @@ __device__ __forceinline__ void short_pairs(const ExpandArgs& a, LDS& L, u64 mp,
     short_pairs_n<W, MODE, ALIVE, GP_ROWS_IN_FLIGHT>(a, L, mp, base, slot_of, st, ee);
 }
 
+// Done in-neighbours (a.dbits rounds: early exit, no liveness,
+// one context).  Without liveness a receiver's new bits are OR_u seen(u) &
+// ~seen(v) over all its in-neighbours (ExpandArgs), and every Message-List is
+// a subset of the component's messages cmask, so one in-neighbour that held
+// all of them at the end of the last round makes the result exactly cmask &
+// ~seen(v): the receiver takes the early-exit target and gathers no row.
+// Probed for the first GP_DNB_K arcs of the gather order (the biggest
+// neighbours, the first to complete), all loads in flight together.  (Not in
+// the flat kernel: its 2-arc prefix pass already reads those rows, and the
+// extra probe round trip made the 512-message shard's rounds slower.)
+#ifndef GP_DNB_K
+#define GP_DNB_K 2
+#endif
+__device__ __forceinline__ bool done_nb(const ExpandArgs& a, int64_t b, int64_t e) {
+  int32_t c[GP_DNB_K];
+#pragma unroll
+  for (int q = 0; q < GP_DNB_K; ++q) c[q] = b + q < e ? a.gcol[b + q] : -1;
+  u64 w[GP_DNB_K];
+#pragma unroll
+  for (int q = 0; q < GP_DNB_K; ++q) w[q] = c[q] >= 0 ? a.dbits[c[q] >> 6] : 0ull;
+  bool d = false;
+#pragma unroll
+  for (int q = 0; q < GP_DNB_K; ++q) d = d || (c[q] >= 0 && ((w[q] >> (c[q] & 63)) & 1ull));
+  return d;
+}
+
+// Receivers with a done in-neighbour two at a time, one per half-wave (W =
+// 64): nothing to gather, so each pair is one round trip (its seen rows and
+// the component rows, the latter L2-resident) and the commit
+#ifndef GP_DNB_PAIRS
+#define GP_DNB_PAIRS 1
+#endif
+template <int W, class LDS>
+__device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
+                                          WaveStats& st) {
+  static_assert(W == 64, "half-wave rows");
+  const int lane = threadIdx.x & 63, h = lane >> 5, lw = lane & 31;
+  while (mp) {
+    const int kA = __ffsll((long long)mp) - 1;
+    mp &= mp - 1;
+    int kB = -1;
+    if (mp) {
+      kB = __ffsll((long long)mp) - 1;
+      mp &= mp - 1;
+    }
+    const bool on = h == 0 || kB >= 0;
+    const int ks = (h && kB >= 0) ? kB : kA;
+    const int64_t i = base + ks;
+    const int v = (int)(a.vbegin + i);
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
+    u64x2 sv = {0, 0}, cm = {0, 0};
+    if (on) {
+      if (sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
+      cm = load_piece<W>(a.cmask, L.mi[ks], lw);
+    }
+    const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
+    const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
+    st.add(S_SEEN_READ, (u64)((sA != SLOT_NONE ? 1 : 0) + (kB >= 0 && sB != SLOT_NONE ? 1 : 0)));
+    pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, cm, sv, st);
+  }
+}
+
 // k_expand's commit of the deferred per-vertex words: lane k holds vertex
 // base + k (need: it was scanned)
 template <class LDS>
@@ -1036,7 +1100,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
   const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
   if (base < a.nloc) {
     const int64_t li = base + lane;
-    bool need = false, act = false;
+    bool need = false, act = false, dnb = false;
     u64 sends = 0;
     uint32_t slot_of = SLOT_NONE;
     uint32_t pre_arcs = 0;   // SCAN_PRE: arcs the lane phase scanned
@@ -1099,6 +1163,7 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       if (!need && !hub) a.fpop_next[v] = 0;
       slot_of = a.sp[v];
       if (a.early_exit && need) L.mi[lane] = a.midx[v];
+      if (a.dbits && need) dnb = done_nb(a, b, e);
     }
     if constexpr ((MODE & 3) == SCAN_PRE) st.add(S_ARCS, (u64)wave_sum_u32(pre_arcs));
     st.add(S_SENDS, wave_sum_u64(sends));
@@ -1110,6 +1175,8 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
     wave_sync_lds();
     const bool ee = a.early_exit != 0;
     u64 m = __ballot(need);
+    const u64 mdn = __ballot(dnb);   // receivers with a done in-neighbour (a.dbits rounds)
+    st.add(S_DNB, (u64)__popcll(mdn));
     if constexpr ((MODE & 3) == SCAN_PRE && GP_WAVE_PRE_MAX > PRE_MAX_DEG) {
       // receivers with PRE_MAX_DEG < deg <= GP_WAVE_PRE_MAX: the wave probes
       // their in-lists GP_WAVE_PRE_N at a time (one coalesced pass each, all
@@ -1174,6 +1241,13 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
         m &= ~mp;
       }
     }
+    if constexpr (W == 64 && GP_DNB_PAIRS) {
+      if (mdn) {   // done in-neighbours: two receivers at a time, the rest below
+        const u64 md = m & mdn;
+        dnb_pairs<W>(a, L, md, base, slot_of, st);
+        m &= ~md;
+      }
+    }
     if constexpr ((GP_SHORT_PAIRS || PAIRS) && W == 64 && (MODE & 3) != SCAN_MASKED) {
       bool pairs = true;   // (record rounds read records in the single-receiver scan)
       if constexpr ((MODE & SCAN_CML) != 0) pairs = a.cmk == nullptr;
@@ -1200,6 +1274,8 @@ __global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
       // component already: then there is nothing to scan)
       if (ALIVE && ee && a.alive && !__any((want.x | want.y) != 0ull)) {
         if (a.sate) sat |= 1ull << k;
+      } else if ((mdn >> k) & 1ull) {   // a done in-neighbour: its Message-List is the whole target
+        acc = want;
       } else if constexpr ((MODE & 3) == SCAN_PRE) {
         const uint32_t np = L.np[k];
         if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
@@ -2188,15 +2264,28 @@ __global__ __launch_bounds__(BLOCK) void k_apply_lanes(ExpandArgs a) {
   flush_stats(st, a.partial);
 }
 
-// frontier activity bitmap: bit v = (fpop[v] != 0), one word per 64 vertices
+// frontier activity bitmap: bit v = (fpop[v] != 0), one word per 64 vertices.
+// With dbits (single context, early-exit round without liveness) also the done
+// bitmap: bit v = v holds every message of its component (seenpop == done_at,
+// components with messages only), as of the end of the last round.
 __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, u64* __restrict__ abits,
-                                                  int64_t n) {
+                                                  int64_t n, const uint32_t* __restrict__ seenpop,
+                                                  const uint32_t* __restrict__ done_at, u64* __restrict__ dbits) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
     const int64_t v = v0 + lane;
     const u64 m = __ballot(v < n && fpop[v] != 0u);
     if (lane == 0) abits[v0 >> 6] = m;
+    if (dbits) {
+      bool d = false;
+      if (v < n) {
+        const uint32_t t = done_at[v];
+        d = t != 0u && seenpop[v] == t;
+      }
+      const u64 dm = __ballot(d);
+      if (lane == 0) dbits[v0 >> 6] = dm;
+    }
   }
 }
 
@@ -3092,6 +3181,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.fpop = c->d_fpop[c->cur];
   a.abits = c->d_abits;
   a.sbits = c->sum_now ? c->d_sbits : nullptr;
+  a.dbits = c->dnb_now ? c->d_dbits : nullptr;
   a.amask = c->d_amask;
   a.cmk = c->cml_read_now ? c->d_cmk[c->cur] : nullptr;
   a.cml = c->cml_read_now ? c->d_cml[c->cur] : nullptr;
@@ -3295,8 +3385,6 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 static int launch_expand(Ctx* c) {
   if (alive_on(c))   // F_{r+1} is built by this round's receivers
     GP_HIP(hipMemsetAsync(c->d_alive + (size_t)(c->cur ^ 1) * c->words, 0, (size_t)c->words * 8, c->stream));
-  hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
-                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc);
   // direction: push when the senders' arcs are a small share of all arcs
   const int r = c->round;
   // early exit pays once frontier rows are dense: >= m/16 new bits per vertex last round
@@ -3345,6 +3433,21 @@ static int launch_expand(Ctx* c) {
       }
     }
   }
+  // done in-neighbours: without liveness a receiver with an
+  // in-neighbour that held its whole component at the end of the last round
+  // receives exactly cmask & ~seen.  Pull rounds of the per-receiver kernel
+  // once most messages are held (before that hardly any vertex is done, and
+  // the probes only cost); the done bitmap comes with the activity bitmap (one
+  // context: seenpop and done_at share the vertex index)
+#ifndef GP_DONE_NB
+#define GP_DONE_NB 1
+#endif
+  c->dnb_now = GP_DONE_NB && c->early_exit_now && !c->mode_push && !c->liveness_active && !c->local &&
+               c->nloc() == c->n_alloc && c->words > c->cfg.flat_max_words &&
+               (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m;
+  hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
+                     dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc,
+                     c->d_seenpop, c->d_done_at, c->dnb_now ? c->d_dbits : nullptr);
   // filtered pull: probe every arc inside the scan, or build the per-arc mask
   // first (pays once the probes are many: senders >= arc_mask_permille of n)
   c->arc_mask_now = !c->mode_push && !c->unfiltered_now && c->cfg.arc_mask_permille > 0 &&
@@ -3510,7 +3613,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_det_big); dfree(&c->d_det_pre); dfree(&c->d_det_live); dfree(&c->d_det_cur); dfree(&c->d_det_base);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
@@ -3619,6 +3722,7 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_det_cur, (size_t)DET_CAP));
   GP_TRY(dalloc(&c->d_det_base, (size_t)DET_CAP));
   GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
+  GP_TRY(dalloc(&c->d_dbits, (na + 63) / 64));
 #if GP_SUMMARY_PROBE
   GP_TRY(dalloc(&c->d_sbits, (na + 4095) / 4096));
 #endif
@@ -3803,7 +3907,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
@@ -4262,6 +4366,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->overflow = (int64_t)h[S_REPORT_CURSOR] > c->report_cap ? 1 : 0;
     out->xchg_rows = h[S_XROWS];
     out->xchg_bytes = h[S_XBYTES];
+    out->done_nb = h[S_DNB];
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
     out->expand_ms = ms;
@@ -4328,7 +4433,7 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     sum.rows_written += st.rows_written; sum.vertices_visited += st.vertices_visited;
     sum.atomics += st.atomics; sum.next_arcs += st.next_arcs; sum.mode = st.mode;
     sum.row_bytes += st.row_bytes; sum.scan = st.scan;
-    sum.xchg_rows += st.xchg_rows; sum.xchg_bytes += st.xchg_bytes;
+    sum.xchg_rows += st.xchg_rows; sum.xchg_bytes += st.xchg_bytes; sum.done_nb += st.done_nb;
     sum.expand_ms = std::max(sum.expand_ms, st.expand_ms);
     sum.exchange_ms = std::max(sum.exchange_ms, st.exchange_ms);
     sum.round_ms = std::max(sum.round_ms, st.round_ms);

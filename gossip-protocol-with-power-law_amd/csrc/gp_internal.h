@@ -24,6 +24,7 @@ enum StatSlot {
   S_REPORTS, S_REMOVALS, S_DUP, S_ARCS, S_GATHERED, S_SEEN_READ, S_WRITTEN,
   S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_ROW_BYTES,
   S_XROWS, S_XBYTES,   // boundary entries / bytes sent (vertex partition, written by the pack step)
+  S_DNB,               // receivers completed from a done in-neighbour (k_expand)
   NST,
   S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR, S_DET_BIG
 };
@@ -142,6 +143,11 @@ struct Ctx {
   u64* d_nbits = nullptr;           // [n_alloc/64] narrow push rounds: receivable vertices (k_mkneed)
   u64* d_abits = nullptr;
   u64* d_sbits = nullptr;   // summary level of d_abits (GP_SUMMARY_PROBE builds)
+  // [n_alloc/64] done bitmap of early-exit rounds without liveness (single
+  // context): bit v = v held every message of its component at the end of the
+  // last round (done in-neighbours)
+  u64* d_dbits = nullptr;
+  bool dnb_now = false;             // this round's pull reads d_dbits
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
   u64* d_amask = nullptr;
   // push (sparse-round) mode

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 13
+#define GP_ABI_VERSION 14
 
 typedef struct gp_ctx gp_ctx;
 
@@ -92,6 +92,8 @@ typedef struct gp_round_stats {
   double kernel_ms;         /* device time of the pull kernel + its hub passes       */
   uint64_t xchg_rows;       /* vertex partition: boundary entries sent (all peers)   */
   uint64_t xchg_bytes;      /* vertex partition: bytes sent (entry heads + words)    */
+  uint64_t done_nb;         /* receivers that took every message of their component
+                               from an in-neighbour holding all of them (§3.4)      */
 } gp_round_stats;
 
 /* One dead-node report: reporter saw `dead` miss 3 heartbeats in `round`. */

@@ -687,6 +687,25 @@ def test_wide_rows_no_churn(pkg, oracle, mode):
     eng.close()
 
 
+@pytest.mark.parametrize("m,flat_max_words", [(4096, 16), (2048, 16), (512, 0), (64, 0)])
+def test_done_in_neighbours(pkg, oracle, m, flat_max_words):
+    """Late early-exit rounds without liveness: a receiver whose first in-arcs
+    (gather order, hubs first) come from a vertex that held its whole component
+    at the end of the last round takes cmask & ~seen without gathering a row
+    (done_nb counts them; W = 64 two per wave-instruction, narrower rows in the
+    per-receiver kernel's serial loop).  Bit-exact against the oracle,
+    first-receipt matrix included."""
+    rp, col = oracle.chung_lu(150_000, 12, 2.5, 41)
+    g = pkg.CSR(150_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, m, seed=41)
+    r = _compare(pkg, oracle, g, origin, flat_max_words=flat_max_words)
+    dnb = [s["done_nb"] for s in r["stats"]]
+    assert sum(dnb) > 0, dnb
+    for s in r["stats"]:   # only pulls of rounds once most messages are held
+        assert s["done_nb"] == 0 or (s["mode"] == 0 and s["done_nb"] <= s["vertices_visited"])
+    r["eng"].close()
+
+
 @pytest.mark.parametrize("prefilter", [0, 20])
 @pytest.mark.parametrize("churn", [False, True])
 def test_compact_message_lists(pkg, oracle, prefilter, churn):
