@@ -57,6 +57,10 @@ def parse():
                     help="sparse probe rounds of overlays with >= this many vertices read the summary level first")
     ap.add_argument("--flat-max-words", type=int, default=16,
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
+    ap.add_argument("--message-order", choices=("given", "spread"), default="spread",
+                    help="bit order of the message table: as drawn, or grouped by spread speed "
+                         "(overlay.spread_order)")
+    ap.add_argument("--spread-hops", type=int, default=3, help="--message-order spread: key radius (1..3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-log2n", type=int, default=None,
@@ -110,7 +114,7 @@ def pmc_traffic(config):
     gfx950 correction of MI355X_MICROARCH.md), from the profiles/pmc_traffic*.json
     whose workload keys match this run (C4: pmc_traffic.json, C5:
     pmc_traffic_c5.json); None when no such measurement is committed."""
-    keys = ("n", "arcs", "messages", "words_per_row", "seed", "parallelism")
+    keys = ("n", "arcs", "messages", "words_per_row", "seed", "parallelism", "message_order")
     for path in PMC_TRAFFIC:
         try:
             d = json.load(open(path))
@@ -231,10 +235,16 @@ def main():
     deg = eng.check_degree(args.gamma)
     t0 = time.perf_counter()
     shards = world > 1 and args.parallel == "messages"
+    origin = pkg.overlay.random_origins(n, args.messages, seed=args.seed)
+    if args.message_order == "spread":   # bit order by spread speed; setup, untimed
+        # within each rank's shard, so that every rank gets messages of every speed
+        blocks = ([dist.message_shard(args.messages, world, p) for p in range(world)] if shards
+                  else [(0, args.messages)])
+        origin = np.concatenate([origin[lo:hi][eng.spread_order(origin[lo:hi], hops=args.spread_hops)]
+                                 for lo, hi in blocks])
     if world > 1 and not shards:
         eng.set_partition(rank, world)
         eng.comm_init(dist.share_comm_id(pg, pkg.GossipEngine.comm_unique_id), world, rank)
-    origin = pkg.overlay.random_origins(n, args.messages, seed=args.seed)
     if shards:   # this rank's word-aligned block of the 4096 messages
         lo, hi = dist.message_shard(args.messages, world, rank)
         eng.set_message_shard(origin, None, lo, hi)
@@ -308,6 +318,8 @@ def main():
                                     "C4: Chung-Lu gamma=2.5 overlay, full forward-once gossip run"),
                        "n": n, "arcs": nnz, "mean_degree": nnz / n, "messages": args.messages,
                        "words_per_row": eng.words, "rounds_per_step": rounds / args.steps,
+                       "message_order": (f"spread ({args.spread_hops}-hop key)" if args.message_order == "spread"
+                                         else "given"),
                        "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,
                        "parallelism": (f"message-shard x{world} (no data-path collective)" if shards else
                                        f"vertex-partition x{world}" + (" (sparse boundary exchange, ncclSend/Recv)"

@@ -111,6 +111,7 @@ SIGNATURES = {
     "gp_comm_unique_id": (ctypes.c_int, [_P]),
     "gp_comm_init": (ctypes.c_int, [_P, _P, _I32, _I32]),
     "gp_set_messages": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "gp_spread_keys": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     "gp_crash": (ctypes.c_int, [_P, _I32, _P]),
     "gp_reset": (ctypes.c_int, [_P]),
     "gp_round": (ctypes.c_int, [_P, ctypes.POINTER(RoundStats)]),
@@ -127,7 +128,7 @@ SIGNATURES = {
     "gp_checkpoint_load": (ctypes.c_int, [_P, _P, _I64]),
 }
 
-ABI_VERSION = 14   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 15   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

@@ -3150,6 +3150,28 @@ __global__ void k_degree(const int64_t* __restrict__ rp, int32_t* __restrict__ d
   if (v < n) deg[v] = (int32_t)(rp[v + 1] - rp[v]);
 }
 
+// spread keys (gp_spread_keys): out[k] = sum over the in-list of vtx[k] of
+// val[u] (val null: the degree of u).  One wave per listed vertex, grid-stride
+// over the list; hubs' lists are long, so lanes stride their arcs.
+__global__ __launch_bounds__(BLOCK) void k_nbsum(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                 const u64* __restrict__ val, const int32_t* __restrict__ vtx,
+                                                 int64_t cnt, u64* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (BLOCK / 64);
+  for (int64_t k = (int64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6); k < cnt; k += nw) {
+    const int64_t v = vtx ? vtx[k] : k;
+    const int64_t b = rp[v], e = rp[v + 1];
+    u64 s = 0;
+    for (int64_t j = b + lane; j < e; j += 64) {
+      const int32_t u = col[j];
+      s += val ? val[u] : (u64)(rp[u + 1] - rp[u]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) out[k] = s;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 
@@ -4114,6 +4136,51 @@ int gp_set_messages(gp_ctx* c, int32_t m, const int32_t* origin, const int32_t* 
   c->h_inj_origin = g_origin;
   c->h_inj_bits = g_bits;
   c->done_at_valid = false;
+  return 0;
+}
+
+int gp_spread_keys(gp_ctx* c, int32_t hops, int32_t m, const int32_t* origin, uint64_t* keys_out) {
+  if (!c) return set_error(GP_EINVAL, "null ctx");
+  if (c->n <= 0 || !c->d_row_ptr || !c->d_col || c->local)
+    return set_error(GP_ESTATE, "gp_spread_keys needs the global overlay (before a vertex partition)");
+  if (hops < 1 || hops > 3) return set_error(GP_EINVAL, "hops must be 1, 2 or 3");
+  if (m < 0 || (m > 0 && (!origin || !keys_out))) return set_error(GP_EINVAL, "bad message table");
+  if (m == 0) return 0;
+  for (int32_t k = 0; k < m; ++k)
+    if (origin[k] < 0 || origin[k] >= c->n) return set_error(GP_EINVAL, "origin out of range");
+  GP_HIP(hipSetDevice(c->device));
+  std::vector<u64> keys((size_t)m);
+  if (hops == 1) {
+    std::vector<int64_t> rp(2);
+    for (int32_t k = 0; k < m; ++k) {
+      GP_TRY(copy_sync(c, rp.data(), c->d_row_ptr + origin[k], 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+      keys[(size_t)k] = (u64)(rp[1] - rp[0]);
+    }
+  } else {
+    int32_t* d_o = nullptr;
+    u64 *d_k = nullptr, *d_s2 = nullptr;
+    GP_HIP(hipMalloc(&d_o, (size_t)m * sizeof(int32_t)));
+    GP_HIP(hipMalloc(&d_k, (size_t)m * sizeof(u64)));
+    int rc = copy_sync(c, d_o, origin, (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (rc == 0 && hops == 3 && hipMalloc(&d_s2, (size_t)c->n * sizeof(u64)) != hipSuccess)
+      rc = set_error(GP_ENOMEM, "gp_spread_keys: n u64 of scratch");
+    if (rc == 0) {
+      // grid-stride kernel: at most 64 K blocks (n / 4 blocks of 256 threads
+      // would overflow the 2^32-thread grid at 2^26 vertices)
+      if (hops == 3)   // hops-2 key of every vertex, then summed over the origins' neighbours
+        hipLaunchKernelGGL(k_nbsum, dim3(std::min(grid_for(c->n, BLOCK / 64), 65536)), dim3(BLOCK), 0, c->stream,
+                           c->d_row_ptr, c->d_col, (const u64*)nullptr, (const int32_t*)nullptr, c->n, d_s2);
+      hipLaunchKernelGGL(k_nbsum, dim3(std::min(grid_for(m, BLOCK / 64), 65536)), dim3(BLOCK), 0, c->stream,
+                         c->d_row_ptr, c->d_col, (const u64*)d_s2, (const int32_t*)d_o, (int64_t)m, d_k);
+      if (hipGetLastError() != hipSuccess) rc = set_error(GP_EHIP, "gp_spread_keys: launch failed");
+      rc = copy_sync(c, keys.data(), d_k, (size_t)m * sizeof(u64), hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d_o);
+    (void)hipFree(d_k);
+    if (d_s2) (void)hipFree(d_s2);
+    if (rc) return rc;
+  }
+  std::memcpy(keys_out, keys.data(), (size_t)m * sizeof(u64));
   return 0;
 }
 

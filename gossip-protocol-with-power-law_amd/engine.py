@@ -162,6 +162,21 @@ class GossipEngine:
         self.inject_round = r if r is not None else np.zeros_like(o)
         _, _, self.m, self.words = self.info()
 
+    def spread_keys(self, origin, hops=2):
+        """gp_spread_keys: arc endpoints within `hops` of each origin (the
+        global overlay; call before a vertex partition)."""
+        o = np.ascontiguousarray(origin, dtype=np.int32)
+        keys = np.zeros(o.size, np.uint64)
+        check(self._lib.gp_spread_keys(self._ctx, int(hops), int(o.size), _ptr(o), _ptr(keys)))
+        return keys
+
+    def spread_order(self, origin, inject_round=None, hops=2):
+        """Permutation p that orders a message table by spread speed
+        (overlay.spread_order): run origin[p] (and inject_round[p]); per-message
+        outputs of that run are those of message p[k] at index k."""
+        from .overlay import spread_order
+        return spread_order(self.spread_keys(origin, hops), inject_round)
+
     def set_message_shard(self, origin, inject_round, lo, hi):
         """Take messages [lo, hi) of a larger message table as this context's
         shard: local message k is global message lo + k.  lo must

@@ -229,3 +229,36 @@ def barabasi_albert(n, m, seed):
 def random_origins(n, m, seed):
     """Message origins of the throughput configs: PCG64(seed + 100), SURVEY.md §8d."""
     return np.random.Generator(np.random.PCG64(seed + 100)).integers(0, n, m).astype(np.int32)
+
+
+def spread_keys(row_ptr, col, origin, hops=2):
+    """Host restatement of gp_spread_keys (DESIGN.md §3.4 "message order"):
+    arc endpoints within `hops` of each origin -- 1: its degree, 2: the sum of
+    its neighbours' degrees, 3: the sum over its neighbours of their hops-2
+    key.  u64, exact."""
+    rp = np.asarray(row_ptr, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    o = np.asarray(origin, dtype=np.int64)
+    if hops not in (1, 2, 3):
+        raise ValueError("hops must be 1, 2 or 3")
+    val = np.diff(rp).astype(np.uint64)
+    for _ in range(hops - 2):   # val <- per-vertex sum of val over the in-list
+        val = np.add.reduceat(np.append(val[col], np.uint64(0)), np.minimum(rp[:-1], col.size)) * (np.diff(rp) > 0)
+        val = val.astype(np.uint64)
+    if hops == 1:
+        return val[o]
+    return np.array([val[col[rp[v]:rp[v + 1]]].sum(dtype=np.uint64) for v in o], dtype=np.uint64)
+
+
+def spread_order(keys, inject_round=None):
+    """Bit order of a message table that groups messages by how fast they
+    spread (DESIGN.md §3.4 "message order"): by inject round, then by spread
+    key descending (gp_spread_keys), ties by index.  Messages from
+    well-connected origins complete early and then share 128-B lines of the
+    Message-List rows, which the late early-exit rounds skip whole.  Returns
+    the permutation p: message k of the ordered table is message p[k] of the
+    given one."""
+    keys = np.asarray(keys, dtype=np.float64)
+    idx = np.arange(keys.size)
+    r = np.zeros(keys.size, np.int64) if inject_round is None else np.asarray(inject_round, np.int64)
+    return np.lexsort((idx, -keys, r))

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 14
+#define GP_ABI_VERSION 15
 
 typedef struct gp_ctx gp_ctx;
 
@@ -196,6 +196,18 @@ int gp_comm_init(gp_ctx* ctx, const void* unique_id128, int32_t nranks, int32_t 
 /* Messages: origin vertex and inject round of each message (Peer.py:397-399:
  * message #n of a peer is its n-th generated gossip). */
 int gp_set_messages(gp_ctx* ctx, int32_t m, const int32_t* origin, const int32_t* inject_round);
+
+/* Spread keys of candidate origins, for ordering a message table before
+ * gp_set_messages (DESIGN.md §3.4 "message order"; no reference counterpart:
+ * the reference's Message-List is an unordered set of strings, Peer.py:175-216,
+ * so the bit position of a message is the engine's choice).  keys_out[k] is the
+ * number of arc endpoints within `hops` (1..3) of origin[k]: hops 1 = degree,
+ * 2 = the sum of its neighbours' degrees, 3 = the sum over its neighbours of
+ * their hops-2 key.  Messages whose keys are close spread at similar speed, so
+ * placing them in adjacent bits lets the late early-exit rounds skip whole
+ * 128-B lines of Message-List rows.  Needs the global overlay (before
+ * gp_set_partition with nranks > 1). */
+int gp_spread_keys(gp_ctx* ctx, int32_t hops, int32_t m, const int32_t* origin, uint64_t* keys_out);
 
 /* Explicit crash injection (the reference's silent mode, Peer.py:437-439),
  * applied at the start of the next round in addition to random churn. */

@@ -5,7 +5,8 @@ messages.  C5: the C4 recipe at 2^26 vertices (seed 5) with 1 %/round crashes,
 3-miss liveness detection and seed removal (Peer.py:298-313, Seed.py:358-406).
 
 C4: the oracle (oracle/gossip_oracle.c, OpenMP) runs ALL 4096 messages (W = 64,
-the bench's configuration) on the overlay the device built, and the engine's
+the bench's configuration: its message table in spread order) on the overlay
+the device built, and the engine's
 whole run must equal it output for output: per-round counters, the Message-List
 of every vertex, digests, per-message coverage and forwards.  The receive /
 forward logic restated is Peer.py:175-216, 395-408 plus forward-once
@@ -123,6 +124,7 @@ def _full_size(pkg, oracle, log2n, seed, churn):
     assert chk["ok"], chk
     g = whole.graph()
     origin = pkg.overlay.random_origins(n, m, seed=seed)
+    origin = origin[whole.spread_order(origin, hops=3)]   # the bench's message order
 
     # the bench's configuration: all 4096 messages, W = 64
     t0 = time.time()

@@ -706,6 +706,57 @@ def test_done_in_neighbours(pkg, oracle, m, flat_max_words):
     r["eng"].close()
 
 
+@pytest.mark.parametrize("hops", [1, 2, 3])
+def test_spread_keys_match_host(pkg, oracle, hops):
+    """gp_spread_keys (device) equals overlay.spread_keys (host), u64-exact, on
+    a Chung-Lu overlay with hubs, repeated origins and isolated vertices."""
+    rp, col = oracle.chung_lu(80_000, 10, 2.3, 44)
+    g = pkg.CSR(80_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 3000, seed=44)
+    origin[:5] = np.argsort(-np.diff(rp))[:5]                # the top hubs
+    iso = np.nonzero(np.diff(rp) == 0)[0]
+    if iso.size:
+        origin[5] = iso[0]
+    origin[6] = origin[7]
+    with pkg.GossipEngine(0) as eng:
+        eng.load_graph(g)
+        assert np.array_equal(eng.spread_keys(origin, hops), pkg.overlay.spread_keys(rp, col, origin, hops))
+        with pytest.raises(pkg.GossipError):
+            eng.spread_keys(origin, 4)
+
+
+@pytest.mark.parametrize("mode", [MODES[0], MODES[2], MODES[4]], ids=["pull", "pull-unfiltered", "adaptive"])
+@pytest.mark.parametrize("churn", [False, True])
+def test_spread_order_is_a_relabelling(pkg, oracle, mode, churn):
+    """The spread order only relabels messages: the engine's
+    run of the ordered table equals the oracle's run of that table (first
+    matrix, digests, counters), and its per-message outputs are those of the
+    given order, permuted -- coverage, forwards and first-matrix columns; sends
+    and receipts per round are unchanged.  Late rounds load fewer row bytes."""
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
+    rp, col = oracle.chung_lu(120_000, 12, 2.5, 45)
+    g = pkg.CSR(120_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 4096, seed=45)
+    kw = dict(churn=True, p_fail=0.01, churn_seed=5) if churn else {}
+    base = _compare(pkg, oracle, g, origin, first=True, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct,
+                    flat_max_words=flat_max_words, arc_mask_permille=arc_mask, **kw)
+    perm = base["eng"].spread_order(origin)
+    assert sorted(perm.tolist()) == list(range(origin.size)) and not np.array_equal(perm, np.arange(origin.size))
+    ordered = _compare(pkg, oracle, g, origin[perm], first=True, push_ratio=push_ratio,
+                       unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask,
+                       **kw)
+    a, b = base["eng"], ordered["eng"]
+    assert [s["new_bits"] for s in base["stats"]] == [s["new_bits"] for s in ordered["stats"]]
+    assert [s["sends"] for s in base["stats"]] == [s["sends"] for s in ordered["stats"]]
+    assert np.array_equal(b.coverage(), a.coverage()[perm])
+    assert np.array_equal(b.forwards(), a.forwards()[perm])
+    assert np.array_equal(b.first(), a.first()[:, perm])
+    if not churn and unfiltered_pct == 90:
+        assert sum(s["row_bytes"] for s in ordered["stats"]) < sum(s["row_bytes"] for s in base["stats"])
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("prefilter", [0, 20])
 @pytest.mark.parametrize("churn", [False, True])
 def test_compact_message_lists(pkg, oracle, prefilter, churn):
