@@ -92,7 +92,8 @@ def round_bytes(st, words, nloc):
     alone (scan 2, unfiltered), the neighbour-row bytes the kernel actually
     loaded (8W per gathered row, less the words early-exit rounds skip), per
     receiver seen row read 8W B and per receiver seen row written to the next
-    slot 8W B."""
+    slot 8W B; plus the senders' rows read to build line masks (k_mklm, 8W B
+    each) before a filtered 64-word pull."""
     w8 = 8 * words
     scan = st.get("scan", 0)
     if scan == 2:
@@ -102,7 +103,7 @@ def round_bytes(st, words, nloc):
     else:
         arcs = 12 * st["arcs_scanned"]
     return (21 * nloc + arcs + st["row_bytes"] + w8 * st["seen_rows_read"]
-            + w8 * st["rows_written"])
+            + w8 * st["rows_written"] + w8 * st.get("lm_rows", 0))
 
 
 PMC_TRAFFIC = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json")))
@@ -293,7 +294,7 @@ def main():
         for s in runs[-1]:
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
-                                                "rows_written", "row_bytes", "atomics", "done_nb",
+                                                "rows_written", "row_bytes", "atomics", "done_nb", "lm_rows",
                                                 "crashed", "reports", "removals", "scan", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None

@@ -57,6 +57,7 @@ class RoundStats(ctypes.Structure):
         ("xchg_rows", ctypes.c_uint64),
         ("xchg_bytes", ctypes.c_uint64),
         ("done_nb", ctypes.c_uint64),
+        ("lm_rows", ctypes.c_uint64),
     ]
 
     def as_dict(self):

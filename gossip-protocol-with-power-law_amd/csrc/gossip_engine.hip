@@ -188,6 +188,7 @@ struct ExpandArgs {
   int32_t sate;                        // alive early-exit round, no injection left: mark sated receivers
   u64* __restrict__ alive_next;        // [W] the same for round r + 1: OR of the new rows (or null)
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
+  const uint8_t* __restrict__ lm;      // SCAN_LINES: line mask of each sender's row (0: inactive)
   const u64* __restrict__ cmk;         // record rounds: dense bitmap of this round's senders (bit v:
                                        //   read v's full row) (or null)
   const u64* __restrict__ cml;         // their records (word 0 mask, then the nonzero words)
@@ -293,6 +294,7 @@ struct WaveLdsT {
   uint8_t cd[CML ? 64 : 1];       // record-writing rounds: vertex k's row is dense (no record)
   int32_t pre[PRE ? 64 : 1][PRE_IDS];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
   uint8_t np[PRE ? 64 : 1];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
+  uint8_t lmv[64];                // SCAN_LINES: line masks of the staged neighbours (L.idx)
   u64 alive[64];                  // OR of the new rows this wave wrote (alive_next)
 };
 using WaveLds = WaveLdsT<false, false>;
@@ -393,7 +395,9 @@ enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PR
                 SCAN_ALIVE = 8 /* flag: early-exit targets narrowed to the alive messages (k_expand);
                                   a variant of its own: +2-3 VGPRs cost a wave per SIMD */,
                 SCAN_PAIRS = 16 /* flag: receivers with short in-lists two at a time (short_pairs,
-                                   W = 64), a variant of its own for the late latency-bound rounds */ };
+                                   W = 64), a variant of its own for the late latency-bound rounds */,
+                SCAN_LINES = 32 /* flag (W = 64, filtered): the probe reads the sender's line mask
+                                   (k_mklm) and the gather loads only its nonzero 128-B lines */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
@@ -458,8 +462,12 @@ __device__ __forceinline__ u64 line_pieces(u64 b) {
 }
 template <int W, int RIF>
 __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
-                                              u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
+                                              u64x2& acc, WaveStats& st, bool ee, u64x2 want,
+                                              const uint8_t* lmk = nullptr) {
   constexpr int RPI = Geo<W>::RPI;
+  // SCAN_LINES (W = 64): lmk[k] names the 128-B lines of row k that hold a
+  // nonzero word (8 lanes x 16 B per line); the others are not loaded
+  const int line = W == 64 ? lw >> 3 : 0;
   bool live = true;   // this lane's words still miss messages
   if (GP_WORD_SKIP && ee) {
     u64x2 t = acc;
@@ -473,14 +481,17 @@ __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t
     for (int q = 0; q < RIF; ++q) {
       const int k = k0 + g + q * RPI;
       r[q] = u64x2{0, 0};
-      if (k < cnt && live) r[q] = load_piece<W>(a.rows, idx[k], lw);
+      if (k < cnt && live && (!lmk || ((lmk[k] >> line) & 1u))) r[q] = load_piece<W>(a.rows, idx[k], lw);
     }
 #pragma unroll
     for (int q = 0; q < RIF; ++q) acc |= r[q];
     st.add(S_GATHERED, (u64)min(RIF * RPI, cnt - k0));
-    u64 pieces = 0;   // 8 * WPL-byte pieces of the lines the loads touched (word skip)
+    u64 pieces = 0;   // 8 * WPL-byte pieces of the lines the loads touched (word skip, line masks)
 #pragma unroll
-    for (int q = 0; q < RIF; ++q) pieces += line_pieces<W>(__ballot(k0 + g + q * RPI < cnt && live));
+    for (int q = 0; q < RIF; ++q) {
+      const int k = k0 + g + q * RPI;
+      pieces += line_pieces<W>(__ballot(k < cnt && live && (!lmk || ((lmk[k] >> line) & 1u))));
+    }
     st.add(S_ROW_BYTES, pieces * (u64)(8 * Geo<W>::WPL));
     if (ee) {
       u64x2 t = acc;
@@ -498,13 +509,14 @@ __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t
 // 64.6 ms per run same-box), the full GP_ROWS_IN_FLIGHT elsewhere
 template <int W>
 __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
-                                            u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
+                                            u64x2& acc, WaveStats& st, bool ee, u64x2 want,
+                                            const uint8_t* lmk = nullptr) {
 #ifndef GP_NEAR_DONE_RIF
 #define GP_NEAR_DONE_RIF 2
 #endif
   if (GP_ROWS_IN_FLIGHT > GP_NEAR_DONE_RIF && a.near_done)
-    return gather_rows_n<W, GP_NEAR_DONE_RIF>(a, idx, cnt, g, lw, acc, st, ee, want);
-  return gather_rows_n<W, GP_ROWS_IN_FLIGHT>(a, idx, cnt, g, lw, acc, st, ee, want);
+    return gather_rows_n<W, GP_NEAR_DONE_RIF>(a, idx, cnt, g, lw, acc, st, ee, want, lmk);
+  return gather_rows_n<W, GP_ROWS_IN_FLIGHT>(a, idx, cnt, g, lw, acc, st, ee, want, lmk);
 }
 
 // position of the k-th (1-based) set bit of m
@@ -609,6 +621,28 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
         wave_sync_lds();
         continue;
       }
+    }
+    if constexpr (W == 64 && (MODE & SCAN_LINES) != 0) {
+      // line masks: the probe reads the sender's byte (0: inactive), the
+      // gather loads only the lines it names
+      uint8_t lv = 0;
+      int32_t u = -1;
+      if (lane < n) {
+        u = a.gcol[j0 + lane];
+        lv = a.lm[u];
+      }
+      const u64 ml = __ballot(lv != 0);
+      if (lv) {
+        const int rk = lane_rank(ml);
+        L.idx[rk] = u;
+        L.lmv[rk] = lv;
+      }
+      wave_sync_lds();
+      if (ml == 0ull) continue;
+      const bool stop = gather_rows<W>(a, L.idx, __popcll(ml), g, lw, acc, st, ee, want, L.lmv);
+      wave_sync_lds();
+      if (stop) break;
+      continue;
     }
     if constexpr ((MODE & 3) == SCAN_MASKED) {
       // the mask names the active arcs: column ids of the others are not loaded
@@ -2289,6 +2323,61 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
   }
 }
 
+// line masks of this round's senders (SCAN_LINES, W = 64): lm[v] = the 128-B
+// lines of v's row in `rows` that hold a nonzero word, 0 for non-senders.  A
+// wave takes 64 vertices; their senders' rows are read two per
+// wave-instruction (a half-wave per row, 8 lanes per line), 4 instructions in
+// flight; the 64 bytes are stored at once
+__global__ __launch_bounds__(BLOCK) void k_mklm(const uint32_t* __restrict__ fpop, const u64* __restrict__ rows,
+                                                int64_t n, uint8_t* __restrict__ lm, u64* __restrict__ partial) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, lw = lane & 31;
+  __shared__ uint8_t s_lm[WAVES][64];
+  uint8_t* out = s_lm[threadIdx.x >> 6];
+  WaveStats st;
+  ws_zero(st);
+  const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
+    const int64_t v = v0 + lane;
+    u64 m = __ballot(v < n && fpop[v] != 0u);
+    st.add(S_LM_ROWS, (u64)__popcll(m));
+    out[lane] = 0;
+    wave_sync_lds();
+    while (m) {
+      int k[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {   // 4 pairs: rows k[2p] (half 0), k[2p + 1] (half 1)
+        k[q] = -1;
+        if (m) {
+          k[q] = __ffsll((long long)m) - 1;
+          m &= m - 1;
+        }
+      }
+      u64x2 r[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int kk = h ? k[2 * p + 1] : k[2 * p];
+        r[p] = kk >= 0 ? load_piece<64>(rows, (int)(v0 + kk), lw) : u64x2{0, 0};
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const u64 b = __ballot((r[p].x | r[p].y) != 0ull);
+        const int kk = h ? k[2 * p + 1] : k[2 * p];
+        if (lw == 0 && kk >= 0) {
+          const uint32_t hb = (uint32_t)(b >> (32 * h));
+          uint8_t l = 0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) l |= ((hb >> (8 * t)) & 0xFFu) ? (uint8_t)(1u << t) : (uint8_t)0;
+          out[kk] = l ? l : (uint8_t)0x0F;   // (a sender whose row reads zero: load it whole)
+        }
+      }
+    }
+    wave_sync_lds();
+    if (v < n) lm[v] = out[lane];
+    wave_sync_lds();
+  }
+  flush_stats(st, partial);
+}
+
 // summary level of the activity bitmap: bit j of sbits[k] = (abits[64k + j] != 0)
 __global__ __launch_bounds__(BLOCK) void k_mksum(const u64* __restrict__ abits, u64* __restrict__ sbits,
                                                  int64_t nwords) {
@@ -3205,6 +3294,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.sbits = c->sum_now ? c->d_sbits : nullptr;
   a.dbits = c->dnb_now ? c->d_dbits : nullptr;
   a.amask = c->d_amask;
+  a.lm = c->lines_now ? c->d_lm : nullptr;
   a.cmk = c->cml_read_now ? c->d_cmk[c->cur] : nullptr;
   a.cml = c->cml_read_now ? c->d_cml[c->cur] : nullptr;
   a.cmk_next = c->cml_write_now ? c->d_cmk[c->cur ^ 1] : nullptr;
@@ -3322,6 +3412,12 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   }
   const int mode = a.unfiltered ? SCAN_UNFILTERED : SCAN_FILTERED;
   (void)hipEventRecord(c->ev[4], c->stream);
+  // line masks of the senders' rows (SCAN_LINES; inside the pull's events and bytes)
+  const bool lines = W == 64 && a.lm != nullptr && !flat && !masked && mode == SCAN_FILTERED && !a.cmk &&
+                     !a.cmk_next && !c->prefilter_now && !(a.alive && a.early_exit);
+  if (lines)
+    hipLaunchKernelGGL(k_mklm, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
+                       dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], a.rows, c->n_alloc, c->d_lm, a.partial);
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
     const dim3 grid(grid_for(a.nloc, (int64_t)WAVES * FlatNR<W>::value));
     if constexpr (W <= 32) {
@@ -3372,6 +3468,12 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
             hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
           else
             hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
+          done = true;
+        }
+      }
+      if constexpr (W == 64) {
+        if (!done && lines) {
+          hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_LINES>), grid, dim3(BLOCK), 0, c->stream, a);
           done = true;
         }
       }
@@ -3500,6 +3602,15 @@ static int launch_expand(Ctx* c) {
     c->cml_read_now = ok && c->cml_written_prev && !c->unfiltered_now && !c->arc_mask_now && !c->early_exit_now;
     c->cml_write_now = ok && sparse && !c->unfiltered_now && !c->arc_mask_now;   // the kernels that write them
   }
+  // line masks (W = 64): a filtered pull without early exit reads its
+  // senders' rows while they are still sparse; their zero 128-B lines are
+  // skipped.  The launch narrows this to the plain
+  // per-receiver kernel (k_expand<64, SCAN_FILTERED | SCAN_LINES>)
+#ifndef GP_LINE_MASKS
+#define GP_LINE_MASKS 1
+#endif
+  c->lines_now = GP_LINE_MASKS && c->words == 64 && c->d_lm != nullptr && !c->mode_push && !c->unfiltered_now &&
+                 !c->arc_mask_now && !c->early_exit_now;
   // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
   c->prefilter_now = !c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.prefilter_pct > 0 &&
                      senders * 100.0 < (double)c->cfg.prefilter_pct * (double)c->n;
@@ -3635,7 +3746,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_det_big); dfree(&c->d_det_pre); dfree(&c->d_det_live); dfree(&c->d_det_cur); dfree(&c->d_det_base);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
@@ -3745,6 +3856,8 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_det_base, (size_t)DET_CAP));
   GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
   GP_TRY(dalloc(&c->d_dbits, (na + 63) / 64));
+  dfree(&c->d_lm);
+  if (c->words == 64) GP_TRY(dalloc(&c->d_lm, na));
 #if GP_SUMMARY_PROBE
   GP_TRY(dalloc(&c->d_sbits, (na + 4095) / 4096));
 #endif
@@ -3929,7 +4042,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
@@ -4434,6 +4547,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->xchg_rows = h[S_XROWS];
     out->xchg_bytes = h[S_XBYTES];
     out->done_nb = h[S_DNB];
+    out->lm_rows = h[S_LM_ROWS];
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
     out->expand_ms = ms;
@@ -4501,6 +4615,7 @@ int gp_round_group(gp_ctx** ctxs, int32_t nctx, gp_round_stats* out) {
     sum.atomics += st.atomics; sum.next_arcs += st.next_arcs; sum.mode = st.mode;
     sum.row_bytes += st.row_bytes; sum.scan = st.scan;
     sum.xchg_rows += st.xchg_rows; sum.xchg_bytes += st.xchg_bytes; sum.done_nb += st.done_nb;
+    sum.lm_rows += st.lm_rows;
     sum.expand_ms = std::max(sum.expand_ms, st.expand_ms);
     sum.exchange_ms = std::max(sum.exchange_ms, st.exchange_ms);
     sum.round_ms = std::max(sum.round_ms, st.round_ms);

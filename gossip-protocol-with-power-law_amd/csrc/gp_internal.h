@@ -25,6 +25,7 @@ enum StatSlot {
   S_VISITED, S_NEXT_ARCS, S_ATOMICS, S_ROW_BYTES,
   S_XROWS, S_XBYTES,   // boundary entries / bytes sent (vertex partition, written by the pack step)
   S_DNB,               // receivers completed from a done in-neighbour (k_expand)
+  S_LM_ROWS,           // senders' rows read by k_mklm to build line masks
   NST,
   S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR, S_DET_BIG
 };
@@ -148,6 +149,11 @@ struct Ctx {
   // last round (done in-neighbours)
   u64* d_dbits = nullptr;
   bool dnb_now = false;             // this round's pull reads d_dbits
+  // [n_alloc] line masks (W = 64): bit l = 128-B line l of v's
+  // row in this round's slot holds a nonzero word; 0 = not a sender.  Built by
+  // k_mklm from the very rows the round's filtered pull reads (SCAN_LINES)
+  uint8_t* d_lm = nullptr;
+  bool lines_now = false;
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
   u64* d_amask = nullptr;
   // push (sparse-round) mode

@@ -94,6 +94,8 @@ typedef struct gp_round_stats {
   uint64_t xchg_bytes;      /* vertex partition: bytes sent (entry heads + words)    */
   uint64_t done_nb;         /* receivers that took every message of their component
                                from an in-neighbour holding all of them (§3.4)      */
+  uint64_t lm_rows;         /* senders' rows read to build line masks before a
+                               filtered 64-word pull (8*W bytes each, §3.2)         */
 } gp_round_stats;
 
 /* One dead-node report: reporter saw `dead` miss 3 heartbeats in `round`. */
