@@ -330,7 +330,7 @@ def main():
                                         "gamma": args.gamma, "ok": bool(deg["ok"])}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": (f"k_expand<{eng.words}>" if eng.words > 32 else
+                         "kernel": (f"k_expand<{eng.words}> (+ k_mklm in line-mask rounds)" if eng.words > 32 else
                                     f"k_expand<{eng.words}> / k_expand_flat<{eng.words}>")
                                    + " + k_hub_partial + k_hub_final per pull launch, HIP events on the "
                                      "engine stream",

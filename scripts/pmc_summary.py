@@ -20,12 +20,13 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-SET = ("k_expand", "k_hub_partial", "k_hub_final")
+SET = ("k_mklm", "k_expand", "k_hub_partial", "k_hub_final")
 
 
 def load(d, counter):
-    """Counter per pull launch: a k_expand* dispatch opens a launch, the hub
-    dispatches after it (before the next k_expand*) add to it."""
+    """Counter per pull launch: a k_expand* dispatch opens a launch unless the
+    line-mask pass k_mklm just opened it (it runs first, inside the pull's
+    events); the hub dispatches after it (before the next pull) add to it."""
     path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     per, kind = {}, {}
     for r in csv.DictReader(open(path)):
@@ -33,13 +34,15 @@ def load(d, counter):
             continue
         k = int(r["Dispatch_Id"])
         per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
-        kind[k] = "k_expand" in r["Kernel_Name"]
+        kind[k] = "mklm" if "k_mklm" in r["Kernel_Name"] else ("pull" if "k_expand" in r["Kernel_Name"] else "hub")
     out = []
+    prev = None
     for k in sorted(per):
-        if kind[k]:
+        if kind[k] == "mklm" or (kind[k] == "pull" and prev != "mklm"):
             out.append(per[k])
         elif out:
             out[-1] += per[k]
+        prev = kind[k]
     return out
 
 
@@ -69,7 +72,7 @@ def main():
     th = sum(x["fetch_GB"] + x["write_GB"] for x in rows)
     tm = sum(x["kernel_ms"] for x in rows)
     print(f"| all {len(rows)} launches | {ta:.2f} | | | {th:.2f} | {th / ta:.3f} | {tm:.2f} | {th / tm:.2f} |")
-    out = {"kernel": "k_expand + k_hub_partial + k_hub_final", "launches": len(rows), "traffic_bytes_per_launch": th * 1e9 / len(rows),
+    out = {"kernel": "k_mklm (line-mask rounds) + k_expand + k_hub_partial + k_hub_final", "launches": len(rows), "traffic_bytes_per_launch": th * 1e9 / len(rows),
            "alg_bytes_per_launch": ta * 1e9 / len(rows), "kernel_ms_per_launch": tm / len(rows),
            "rounds": rows, "config": bench["config"],
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bytes = "

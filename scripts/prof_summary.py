@@ -42,6 +42,9 @@ def main():
     # the engine's kernel_ms HIP events bracket
     sets = {}
     for name, calls, tot, avg, pct in rows:
+        if short(name).endswith("k_mklm"):   # line masks: W = 64 pull rounds only, inside the pull's events
+            sets.setdefault("64", {"launches": 0, "pull_ms": 0.0, "hub_ms": 0.0})["hub_ms"] += tot / 1e6
+            continue
         m = re.search(r"k_(expand_flat|expand|hub_partial|hub_final)<(\d+)", short(name))
         if not m:
             continue
@@ -53,7 +56,7 @@ def main():
             e["hub_ms"] += tot / 1e6
     for w, e in sorted(sets.items()):
         if e["launches"]:
-            print(f"\nroofline kernel set, W = {w}: k_expand* + k_hub_partial + k_hub_final = "
+            print(f"\nroofline kernel set, W = {w}: k_expand* + (k_mklm +) k_hub_partial + k_hub_final = "
                   f"{e['pull_ms']:.3f} + {e['hub_ms']:.3f} ms over {e['launches']} pull launches = "
                   f"{(e['pull_ms'] + e['hub_ms']) / e['launches']:.3f} ms per launch")
 
