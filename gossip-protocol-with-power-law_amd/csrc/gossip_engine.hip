@@ -422,6 +422,16 @@ __device__ __forceinline__ bool mask_any(const u64* __restrict__ amask, int64_t 
   return ((amask[k0] & lo) | (amask[k1] & him)) != 0ull;
 }
 
+// line masks (SCAN_LINES): GP_LM_NIBBLE packs two vertices per byte (v even:
+// low nibble), halving the array the per-arc probe reads (8 MB at 2^24: a
+// byte array's 16 MB missed L2 on most probes, C4 round 2 HBM / alg 1.37)
+#ifndef GP_LM_NIBBLE
+#define GP_LM_NIBBLE 1
+#endif
+__device__ __forceinline__ uint8_t lm_of(const uint8_t* __restrict__ lm, int32_t u) {
+  if constexpr (GP_LM_NIBBLE) return (uint8_t)((lm[u >> 1] >> ((u & 1) * 4)) & 0xF);
+  else return lm[u];
+}
 // neighbour u if its row is read this round, else -1
 template <int MODE>
 __device__ __forceinline__ int32_t probe(const ExpandArgs& a, int32_t u) {
@@ -629,7 +639,7 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
       int32_t u = -1;
       if (lane < n) {
         u = a.gcol[j0 + lane];
-        lv = a.lm[u];
+        lv = lm_of(a.lm, u);
       }
       const u64 ml = __ballot(lv != 0);
       if (lv) {
@@ -2372,7 +2382,12 @@ __global__ __launch_bounds__(BLOCK) void k_mklm(const uint32_t* __restrict__ fpo
       }
     }
     wave_sync_lds();
-    if (v < n) lm[v] = out[lane];
+    if constexpr (GP_LM_NIBBLE) {   // (v0 is a multiple of 64: whole bytes per wave)
+      if (lane < 32 && v0 + 2 * lane < n)
+        lm[(v0 >> 1) + lane] = (uint8_t)(out[2 * lane] | (out[2 * lane + 1] << 4));
+    } else if (v < n) {
+      lm[v] = out[lane];
+    }
     wave_sync_lds();
   }
   flush_stats(st, partial);
@@ -3857,7 +3872,7 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_abits, (na + 63) / 64));
   GP_TRY(dalloc(&c->d_dbits, (na + 63) / 64));
   dfree(&c->d_lm);
-  if (c->words == 64) GP_TRY(dalloc(&c->d_lm, na));
+  if (c->words == 64) GP_TRY(dalloc(&c->d_lm, GP_LM_NIBBLE ? (na + 1) / 2 + 32 : na));
 #if GP_SUMMARY_PROBE
   GP_TRY(dalloc(&c->d_sbits, (na + 4095) / 4096));
 #endif
