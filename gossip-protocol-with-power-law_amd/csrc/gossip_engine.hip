@@ -294,7 +294,6 @@ struct WaveLdsT {
   uint8_t cd[CML ? 64 : 1];       // record-writing rounds: vertex k's row is dense (no record)
   int32_t pre[PRE ? 64 : 1][PRE_IDS];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
   uint8_t np[PRE ? 64 : 1];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
-  uint8_t lmv[64];                // SCAN_LINES: line masks of the staged neighbours (L.idx)
   u64 alive[64];                  // OR of the new rows this wave wrote (alive_next)
 };
 using WaveLds = WaveLdsT<false, false>;
@@ -472,12 +471,8 @@ __device__ __forceinline__ u64 line_pieces(u64 b) {
 }
 template <int W, int RIF>
 __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
-                                              u64x2& acc, WaveStats& st, bool ee, u64x2 want,
-                                              const uint8_t* lmk = nullptr) {
+                                              u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
   constexpr int RPI = Geo<W>::RPI;
-  // SCAN_LINES (W = 64): lmk[k] names the 128-B lines of row k that hold a
-  // nonzero word (8 lanes x 16 B per line); the others are not loaded
-  const int line = W == 64 ? lw >> 3 : 0;
   bool live = true;   // this lane's words still miss messages
   if (GP_WORD_SKIP && ee) {
     u64x2 t = acc;
@@ -491,17 +486,14 @@ __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t
     for (int q = 0; q < RIF; ++q) {
       const int k = k0 + g + q * RPI;
       r[q] = u64x2{0, 0};
-      if (k < cnt && live && (!lmk || ((lmk[k] >> line) & 1u))) r[q] = load_piece<W>(a.rows, idx[k], lw);
+      if (k < cnt && live) r[q] = load_piece<W>(a.rows, idx[k], lw);
     }
 #pragma unroll
     for (int q = 0; q < RIF; ++q) acc |= r[q];
     st.add(S_GATHERED, (u64)min(RIF * RPI, cnt - k0));
-    u64 pieces = 0;   // 8 * WPL-byte pieces of the lines the loads touched (word skip, line masks)
+    u64 pieces = 0;   // 8 * WPL-byte pieces of the lines the loads touched (word skip)
 #pragma unroll
-    for (int q = 0; q < RIF; ++q) {
-      const int k = k0 + g + q * RPI;
-      pieces += line_pieces<W>(__ballot(k < cnt && live && (!lmk || ((lmk[k] >> line) & 1u))));
-    }
+    for (int q = 0; q < RIF; ++q) pieces += line_pieces<W>(__ballot(k0 + g + q * RPI < cnt && live));
     st.add(S_ROW_BYTES, pieces * (u64)(8 * Geo<W>::WPL));
     if (ee) {
       u64x2 t = acc;
@@ -519,14 +511,44 @@ __device__ __forceinline__ bool gather_rows_n(const ExpandArgs& a, const int32_t
 // 64.6 ms per run same-box), the full GP_ROWS_IN_FLIGHT elsewhere
 template <int W>
 __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* idx, int cnt, int g, int lw,
-                                            u64x2& acc, WaveStats& st, bool ee, u64x2 want,
-                                            const uint8_t* lmk = nullptr) {
+                                            u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
 #ifndef GP_NEAR_DONE_RIF
 #define GP_NEAR_DONE_RIF 2
 #endif
   if (GP_ROWS_IN_FLIGHT > GP_NEAR_DONE_RIF && a.near_done)
-    return gather_rows_n<W, GP_NEAR_DONE_RIF>(a, idx, cnt, g, lw, acc, st, ee, want, lmk);
-  return gather_rows_n<W, GP_ROWS_IN_FLIGHT>(a, idx, cnt, g, lw, acc, st, ee, want, lmk);
+    return gather_rows_n<W, GP_NEAR_DONE_RIF>(a, idx, cnt, g, lw, acc, st, ee, want);
+  return gather_rows_n<W, GP_ROWS_IN_FLIGHT>(a, idx, cnt, g, lw, acc, st, ee, want);
+}
+
+// SCAN_LINES rounds (W = 64, filtered, no early exit): staged entries carry the
+// sender's line mask in their low 4 bits ((u << 4) | lines, n <= 2^27), and
+// each lane loads its 16-B piece of a row only when its 128-B line is named.
+// No early-exit state: 64 VGPRs less pressure than gather_rows_n with masks.
+#ifndef GP_LINES_RIF
+#define GP_LINES_RIF 3   // 62 VGPRs, 8 waves per SIMD (4: 66, 7 waves): C4 round 2 14.5 -> 14.1 ms
+#endif
+template <int RIF>
+__device__ __forceinline__ void gather_lines(const ExpandArgs& a, const int32_t* ent, int cnt, int g, int lw,
+                                             u64x2& acc, WaveStats& st) {
+  constexpr int RPI = Geo<64>::RPI;
+  const int32_t lbit = 1 << (lw >> 3);
+  for (int k0 = 0; k0 < cnt; k0 += RIF * RPI) {
+    u64x2 r[RIF];
+    u64 pieces = 0;
+#pragma unroll
+    for (int q = 0; q < RIF; ++q) {
+      const int k = k0 + g + q * RPI;
+      r[q] = u64x2{0, 0};
+      const int32_t e = k < cnt ? ent[k] : 0;
+      const bool on = (e & lbit) != 0;
+      if (on) r[q] = load_piece<64>(a.rows, e >> 4, lw);
+      pieces += line_pieces<64>(__ballot(on));
+    }
+#pragma unroll
+    for (int q = 0; q < RIF; ++q) acc |= r[q];
+    st.add(S_GATHERED, (u64)min(RIF * RPI, cnt - k0));
+    st.add(S_ROW_BYTES, pieces * 16ull);
+  }
 }
 
 // position of the k-th (1-based) set bit of m
@@ -642,16 +664,11 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
         lv = lm_of(a.lm, u);
       }
       const u64 ml = __ballot(lv != 0);
-      if (lv) {
-        const int rk = lane_rank(ml);
-        L.idx[rk] = u;
-        L.lmv[rk] = lv;
-      }
+      if (lv) L.idx[lane_rank(ml)] = (u << 4) | (int32_t)lv;
       wave_sync_lds();
       if (ml == 0ull) continue;
-      const bool stop = gather_rows<W>(a, L.idx, __popcll(ml), g, lw, acc, st, ee, want, L.lmv);
+      gather_lines<GP_LINES_RIF>(a, L.idx, __popcll(ml), g, lw, acc, st);
       wave_sync_lds();
-      if (stop) break;
       continue;
     }
     if constexpr ((MODE & 3) == SCAN_MASKED) {
@@ -3625,7 +3642,7 @@ static int launch_expand(Ctx* c) {
 #define GP_LINE_MASKS 1
 #endif
   c->lines_now = GP_LINE_MASKS && c->words == 64 && c->d_lm != nullptr && !c->mode_push && !c->unfiltered_now &&
-                 !c->arc_mask_now && !c->early_exit_now;
+                 !c->arc_mask_now && !c->early_exit_now && c->n_alloc <= (int64_t(1) << 27);   // (u << 4) | lines
   // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
   c->prefilter_now = !c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.prefilter_pct > 0 &&
                      senders * 100.0 < (double)c->cfg.prefilter_pct * (double)c->n;
