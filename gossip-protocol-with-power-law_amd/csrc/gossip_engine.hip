@@ -266,6 +266,16 @@ constexpr int CML_MAXW = CML_WORDS - 1;   // nonzero words a record holds
 #ifndef GP_ROWS_IN_FLIGHT
 #define GP_ROWS_IN_FLIGHT 4
 #endif
+// 64-word rows (C4 / C5: a wave-instruction moves 1 KB): 3 rows per lane in
+// flight -- fewer rows loaded past an early exit, and the alive variant at 65
+// VGPRs: C4 48.2 -> 46.1 ms, C5 245.7-253.5 -> 238.2-241.4 ms same-box
+// (profiles/r03_ab_rif3.txt); 32-word rows keep 4 (the 2048-message shard ran
+// 37.6 -> 38.2 ms with 3)
+#ifndef GP_ROWS_IN_FLIGHT_64
+#define GP_ROWS_IN_FLIGHT_64 3
+#endif
+template <int W>
+struct RowsInFlight { static constexpr int value = W >= 64 ? GP_ROWS_IN_FLIGHT_64 : GP_ROWS_IN_FLIGHT; };
 
 // per-wave LDS of the pull kernels; the mode-specific arrays take one element
 // when their mode is compiled out (LDS is what bounds the waves per CU)
@@ -515,9 +525,9 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* 
 #ifndef GP_NEAR_DONE_RIF
 #define GP_NEAR_DONE_RIF 2
 #endif
-  if (GP_ROWS_IN_FLIGHT > GP_NEAR_DONE_RIF && a.near_done)
+  if (RowsInFlight<W>::value > GP_NEAR_DONE_RIF && a.near_done)
     return gather_rows_n<W, GP_NEAR_DONE_RIF>(a, idx, cnt, g, lw, acc, st, ee, want);
-  return gather_rows_n<W, GP_ROWS_IN_FLIGHT>(a, idx, cnt, g, lw, acc, st, ee, want);
+  return gather_rows_n<W, RowsInFlight<W>::value>(a, idx, cnt, g, lw, acc, st, ee, want);
 }
 
 // SCAN_LINES rounds (W = 64, filtered, no early exit): staged entries carry the
@@ -1043,10 +1053,10 @@ __device__ __forceinline__ void short_pairs_n(const ExpandArgs& a, LDS& L, u64 m
 template <int W, int MODE, bool ALIVE, class LDS>
 __device__ __forceinline__ void short_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
                                             WaveStats& st, bool ee) {
-  if (GP_ROWS_IN_FLIGHT > GP_NEAR_DONE_RIF && a.near_done)
+  if (RowsInFlight<W>::value > GP_NEAR_DONE_RIF && a.near_done)
     short_pairs_n<W, MODE, ALIVE, GP_NEAR_DONE_RIF>(a, L, mp, base, slot_of, st, ee);
   else
-    short_pairs_n<W, MODE, ALIVE, GP_ROWS_IN_FLIGHT>(a, L, mp, base, slot_of, st, ee);
+    short_pairs_n<W, MODE, ALIVE, RowsInFlight<W>::value>(a, L, mp, base, slot_of, st, ee);
 }
 
 // Done in-neighbours (a.dbits rounds: early exit, no liveness,
@@ -1145,8 +1155,17 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, LDS& L, int
 // with coalesced loads; the wave then scans, one receiver at a time, only the
 // vertices that can still receive something.  Kept lean on registers (7 waves
 // per SIMD): the dense rounds are bound by the rows in flight.
+// waves per SIMD asked of the compiler for the alive early-exit variants (C5's
+// rounds 3-5; 0: the compiler's choice)
+#ifndef GP_ALIVE_WAVES
+#define GP_ALIVE_WAVES 0
+#endif
+template <int MODE>
+struct ExpandWaves {
+  static constexpr int value = (MODE & SCAN_ALIVE) != 0 && GP_ALIVE_WAVES > 0 ? GP_ALIVE_WAVES : 1;
+};
 template <int W, int MODE>
-__global__ EXPAND_BOUNDS void k_expand(ExpandArgs a) {
+__global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::value))) void k_expand(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
   __shared__ LDS_OF(MODE) s_w[WAVES];
   const int lane = threadIdx.x & 63;
