@@ -85,8 +85,10 @@ def parse():
 
 def round_bytes(st, words, nloc):
     """Algorithmic bytes of one expansion launch of the pull:
-    per owned vertex 21 B of vertex state (fpop, deg_live, row_ptr pair, state,
-    seenpop, done_at, slot byte), per scanned arc the 4-B column id + the 8-B
+    per owned vertex 26 B of vertex state read (fpop, deg_live, row_ptr pair,
+    state, seenpop, done_at, slot byte) and its 4-B fpop of the next round
+    written, per receiver 23 B of per-vertex words committed (seenpop 4, slot
+    and written-slot bytes 3, digest read-modify-write 16), per scanned arc the 4-B column id + the 8-B
     activity-bitmap probe (scan 0), or 1 mask bit + the 4-B column id of the
     active arcs only (scan 1, + 8 B of mask words per vertex), or the column id
     alone (scan 2, unfiltered), the neighbour-row bytes the kernel actually
@@ -102,8 +104,8 @@ def round_bytes(st, words, nloc):
         arcs = st["arcs_scanned"] / 8 + 4 * st["rows_gathered"] + 8 * nloc
     else:
         arcs = 12 * st["arcs_scanned"]
-    return (21 * nloc + arcs + st["row_bytes"] + w8 * st["seen_rows_read"]
-            + w8 * st["rows_written"] + w8 * st.get("lm_rows", 0))
+    return (30 * nloc + arcs + st["row_bytes"] + w8 * st["seen_rows_read"]
+            + (w8 + 23) * st["rows_written"] + w8 * st.get("lm_rows", 0))
 
 
 PMC_TRAFFIC = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json")))
