@@ -189,6 +189,8 @@ struct ExpandArgs {
   u64* __restrict__ alive_next;        // [W] the same for round r + 1: OR of the new rows (or null)
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
   const uint8_t* __restrict__ lm;      // SCAN_LINES: line mask of each sender's row (0: inactive)
+  uint8_t* __restrict__ lm_next;       // W = 64 pulls: the same for round r + 1, written by the commits
+                                       //   (nibbles; or null)
   const u64* __restrict__ cmk;         // record rounds: dense bitmap of this round's senders (bit v:
                                        //   read v's full row) (or null)
   const u64* __restrict__ cml;         // their records (word 0 mask, then the nonzero words)
@@ -296,6 +298,7 @@ struct WaveLdsT {
   u64 seen2[64];        // pair paths: the second receiver's seen row
   int32_t idx[64];      // active neighbours of one pass
   uint32_t tot[64];     // k_expand: new bits of the wave's vertex k (committed after the loop)
+  uint8_t lmn[64];      // k_expand: line mask of vertex k's new row (committed with tot)
   u64 dig[64];          // k_expand: digest terms of vertex k
   int64_t rp[65];       // k_expand: row_ptr of the wave's vertices (rp[k], rp[k + 1])
   int32_t mi[64];       // k_expand: component-mask row of vertex k (early-exit rounds)
@@ -440,6 +443,13 @@ __device__ __forceinline__ bool mask_any(const u64* __restrict__ amask, int64_t 
 __device__ __forceinline__ uint8_t lm_of(const uint8_t* __restrict__ lm, int32_t u) {
   if constexpr (GP_LM_NIBBLE) return (uint8_t)((lm[u >> 1] >> ((u & 1) * 4)) & 0xF);
   else return lm[u];
+}
+// 4-bit line mask from a ballot over 32 lanes of 16 B (8 lanes per 128-B line)
+__device__ __forceinline__ uint32_t lines_of(uint32_t b) {
+  uint32_t l = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) l |= ((b >> (8 * t)) & 0xFFu) ? (1u << t) : 0u;
+  return l;
 }
 // neighbour u if its row is read this round, else -1
 template <int MODE>
@@ -789,6 +799,13 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   if constexpr (W == 64 && CMLW) {
     if (a.cml_next) dense = write_rec(a.cml_next, v, g, lw, sv | nw);
   }
+  uint32_t lmn = 0;   // W = 64: the lines of the new row holding a nonzero word (lm_next)
+  if constexpr (W == 64) {
+    if (a.lm_next) {
+      const u64x2 row = sv | nw;
+      lmn = lines_of((uint32_t)__ballot(g == 0 && (row.x | row.y) != 0ull));
+    }
+  }
   if (g == 0) {
     alive_add<W>(a, L, lw, nw);
     store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);   // the whole row: the slot may hold an older one
@@ -815,11 +832,14 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   if constexpr (DEFER) {
     if (lane == 0) {
       L.tot[k] = tot;
+      L.lmn[k] = (uint8_t)lmn;
       if constexpr (CMLW && LDS::kCml) L.cd[k] = dense ? 1 : 0;
     }
   } else {
     if (lane == 0) {
       if (a.cmk_next) set_dense(a.cmk_next, v);
+      // (hub passes: the pull's commit left this vertex's nibble 0)
+      if (W == 64 && a.lm_next && lmn) atomicOr(reinterpret_cast<uint32_t*>(a.lm_next) + (v >> 3), lmn << ((v & 7) * 4));
       a.fpop_next[v] = tot;
       a.seenpop[i] += tot;
       a.sp[v] = (uint8_t)a.wslot;
@@ -893,8 +913,14 @@ __device__ __forceinline__ void pair_finish(const ExpandArgs& a, LDS& L, int h, 
   }
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) t ^= __shfl_xor(t, o);
+  uint32_t lmn = 0;   // lines of the new row holding a nonzero word (lm_next)
+  if (a.lm_next) {
+    const u64x2 row = sv | nw;
+    lmn = lines_of((uint32_t)(__ballot(on && (row.x | row.y) != 0ull) >> (32 * h)));
+  }
   if (lw == 0 && on && tot) {
     L.tot[ks] = tot;
+    L.lmn[ks] = (uint8_t)lmn;
     L.dig[ks] = t;
     if constexpr (LDS::kCml) L.cd[ks] = dense ? 1 : 0;
   }
@@ -1142,6 +1168,11 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, LDS& L, int
     }
   }
   st.add(S_NEXT_ARCS, wave_sum_u64(next_arcs));
+  if (a.lm_next) {   // line masks of the next round's senders, two vertices per byte (hubs: 0 here)
+    const uint32_t nib = (need && L.tot[lane]) ? (uint32_t)L.lmn[lane] : 0u;
+    const uint32_t hi = (uint32_t)__shfl_xor((int)nib, 1);
+    if (!(lane & 1) && li < a.nloc) a.lm_next[li >> 1] = (uint8_t)(nib | (hi << 4));
+  }
   if constexpr (LDS::kCml) {   // the wave's 64 vertices are one word of the dense bitmap
     if (a.cmk_next) {
       const u64 dm = __ballot(!need || L.tot[lane] == 0u || L.cd[lane] != 0);
@@ -1777,6 +1808,7 @@ struct RecLds {
   int8_t sown[64];       // their receiver
   int8_t down[64];
   uint32_t tot[REC_NR];  // pair_finish: new bits of receiver k
+  uint8_t lmn[REC_NR];   // pair_finish: its line mask (record rounds write none: lm_next is null)
   u64 dig[REC_NR];       // its digest terms
   uint8_t cd[REC_NR];    // its new row is dense (no record)
   u64 alive[64];         // alive_add (unused: record rounds run without liveness alive sets too)
@@ -2670,6 +2702,7 @@ struct InjectArgs {
   uint8_t* __restrict__ first;
   u64* __restrict__ digest;
   const uint8_t* __restrict__ state;
+  uint8_t* __restrict__ lm;            // written line masks of this round's senders (or null)
   u64* __restrict__ partial;
   int64_t off, groups;
   int64_t vbegin, vend;                // owned local ids [vbegin, vend); beyond: ghosts / extras
@@ -2709,6 +2742,13 @@ __global__ __launch_bounds__(BLOCK) void k_inject(InjectArgs a) {
         if (has_frx) a.frx[(size_t)o * a.words + lane] = f | b;
       }
       if (a.cmk && lane == 0) set_dense(a.cmk, o);   // a sender this round: its record (if any) is stale
+      if (a.lm) {   // written line masks (64 words): the origin's new row, a superset of its old one
+        const u64 nzb = __ballot(lane < a.words && (s | b) != 0ull);
+        uint32_t nib = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) nib |= ((nzb >> (16 * t)) & 0xFFFFull) ? (1u << t) : 0u;
+        if (lane == 0 && nib) atomicOr(reinterpret_cast<uint32_t*>(a.lm) + (o >> 3), nib << ((o & 7) * 4));
+      }
       if (a.alive && b) atomicOr(a.alive + lane, b);   // injected messages are forwarded this round
       const uint32_t nb = wave_sum_u32((uint32_t)__popcll(b));
       if (lane == 0) {
@@ -3345,7 +3385,8 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.sbits = c->sum_now ? c->d_sbits : nullptr;
   a.dbits = c->dnb_now ? c->d_dbits : nullptr;
   a.amask = c->d_amask;
-  a.lm = c->lines_now ? c->d_lm : nullptr;
+  a.lm = c->lines_now ? (c->lm_written_prev && !alive_on(c) ? c->d_lmw[c->cur] : c->d_lm) : nullptr;
+  a.lm_next = c->lm_write_now ? c->d_lmw[c->cur ^ 1] : nullptr;
   a.cmk = c->cml_read_now ? c->d_cmk[c->cur] : nullptr;
   a.cml = c->cml_read_now ? c->d_cml[c->cur] : nullptr;
   a.cmk_next = c->cml_write_now ? c->d_cmk[c->cur ^ 1] : nullptr;
@@ -3466,7 +3507,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   // line masks of the senders' rows (SCAN_LINES; inside the pull's events and bytes)
   const bool lines = W == 64 && a.lm != nullptr && !flat && !masked && mode == SCAN_FILTERED && !a.cmk &&
                      !a.cmk_next && !c->prefilter_now && !(a.alive && a.early_exit);
-  if (lines)
+  if (lines && a.lm == c->d_lm)   // (the last round's commits did not write them)
     hipLaunchKernelGGL(k_mklm, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
                        dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], a.rows, c->n_alloc, c->d_lm, a.partial);
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
@@ -3662,6 +3703,18 @@ static int launch_expand(Ctx* c) {
 #endif
   c->lines_now = GP_LINE_MASKS && c->words == 64 && c->d_lm != nullptr && !c->mode_push && !c->unfiltered_now &&
                  !c->arc_mask_now && !c->early_exit_now && c->n_alloc <= (int64_t(1) << 27);   // (u << 4) | lines
+  // this round's 64-word pull commits write the next round's masks: one
+  // context without liveness (a crash zeroes a sender's fpop, not its mask;
+  // ghosts' rows come from the exchange), per-receiver kernel, no records
+#ifndef GP_LM_WRITE
+#define GP_LM_WRITE 1
+#endif
+  // (only sparse rounds: a line-mask round follows a round with few new bits,
+  // and early-exit rounds would pay the commits' extra stores for nothing --
+  // C4 rounds 3-4 +0.3 ms when every pull wrote them)
+  c->lm_write_now = GP_LM_WRITE && c->words == 64 && c->d_lmw[0] != nullptr && !c->mode_push &&
+                    !c->early_exit_now && !c->liveness_active && !c->local && !c->cml_read_now &&
+                    !c->cml_write_now;
   // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
   c->prefilter_now = !c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.prefilter_pct > 0 &&
                      senders * 100.0 < (double)c->cfg.prefilter_pct * (double)c->n;
@@ -3797,7 +3850,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_det_big); dfree(&c->d_det_pre); dfree(&c->d_det_live); dfree(&c->d_det_cur); dfree(&c->d_det_base);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_lmw[0]); dfree(&c->d_lmw[1]); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
@@ -3909,6 +3962,10 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_dbits, (na + 63) / 64));
   dfree(&c->d_lm);
   if (c->words == 64) GP_TRY(dalloc(&c->d_lm, GP_LM_NIBBLE ? (na + 1) / 2 + 32 : na));
+  for (int k = 0; k < 2; ++k) {
+    dfree(&c->d_lmw[k]);
+    if (c->words == 64 && GP_LM_NIBBLE) GP_TRY(dalloc(&c->d_lmw[k], (na + 1) / 2 + 64));
+  }
 #if GP_SUMMARY_PROBE
   GP_TRY(dalloc(&c->d_sbits, (na + 4095) / 4096));
 #endif
@@ -4093,7 +4150,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_lmw[0]); dfree(&c->d_lmw[1]); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
@@ -4380,6 +4437,7 @@ int gp_reset(gp_ctx* c) {
   c->held_bits = 0;
   c->cml_written_prev = false;
   c->cml_read_now = c->cml_write_now = false;
+  c->lm_written_prev = c->lm_write_now = false;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
   GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n_alloc * 4, hipMemcpyDeviceToDevice, s));
@@ -4497,6 +4555,7 @@ static int round_launch(Ctx* c) {
     ia.first = c->cfg.track_first ? c->d_first : nullptr;
     ia.digest = c->cfg.track_digest ? c->d_digest : nullptr;
     ia.state = c->d_state;
+    ia.lm = c->lm_written_prev ? c->d_lmw[c->cur] : nullptr;
     ia.partial = partial;
     ia.off = it->second.off;
     ia.groups = it->second.cnt;
@@ -4613,6 +4672,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   c->prev_receivers = h[S_RECEIVERS];
   c->held_bits += h[S_INJECTED] + h[S_NEW_BITS];
   c->cml_written_prev = c->cml_write_now;
+  c->lm_written_prev = c->lm_write_now;
   c->cur ^= 1;
   c->round = r + 1;
   return 0;

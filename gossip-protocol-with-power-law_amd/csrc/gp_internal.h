@@ -154,6 +154,12 @@ struct Ctx {
   // k_mklm from the very rows the round's filtered pull reads (SCAN_LINES)
   uint8_t* d_lm = nullptr;
   bool lines_now = false;
+  // [2][n_alloc / 2] the same masks written by the commits of a 64-word pull
+  // for the next round's senders (nibbles, by round parity like d_fpop): a
+  // line-mask round after such a round (no liveness, one context) probes them
+  // without k_mklm's pass over the senders' rows
+  uint8_t* d_lmw[2] = {nullptr, nullptr};
+  bool lm_write_now = false, lm_written_prev = false;
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
   u64* d_amask = nullptr;
   // push (sparse-round) mode
