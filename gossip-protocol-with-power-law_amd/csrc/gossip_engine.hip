@@ -648,7 +648,10 @@ __device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, L
 // probes, staging, gather
 template <int W, int MODE, class LDS>
 __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int64_t e, LDS& L, int lane,
-                                            int g, int lw, u64x2& acc, WaveStats& st, bool ee, u64x2 want) {
+                                            int g, int lw, u64x2& acc, WaveStats& st, bool ee, u64x2 want,
+                                            int32_t col0 = INT32_MIN) {
+  // col0: this lane's column id of the first pass, when the caller loaded it
+  // early (beside the early-exit target's loads; INT32_MIN: not loaded)
   for (int64_t j0 = b; j0 < e; j0 += 64) {
     const int n = (int)min((int64_t)64, e - j0);
     st.add(S_ARCS, n);
@@ -700,7 +703,7 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
       cnt = __popcll(win);
     } else {
       int32_t ent = -1;
-      if (lane < n) ent = probe<MODE>(a, a.gcol[j0 + lane]);
+      if (lane < n) ent = probe<MODE>(a, (col0 != INT32_MIN && j0 == b) ? col0 : a.gcol[j0 + lane]);
       cnt = stage_pass(L, ent);
       if (cnt == 0) continue;
     }
@@ -1377,6 +1380,15 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
       const int64_t vb = L.rp[k], ve = L.rp[k + 1];   // staged by the lane phase
       const uint32_t sv_slot = (uint32_t)__builtin_amdgcn_readlane((int)slot_of, k);
       u64x2 acc = {0, 0}, want = {0, 0};
+      // early-exit rounds: the first pass's column ids are loaded beside the
+      // target's seen / component rows, one round trip instead of two
+#ifndef GP_COL_EARLY
+#define GP_COL_EARLY 1
+#endif
+      int32_t col0 = INT32_MIN;
+      if constexpr (GP_COL_EARLY && (MODE & 3) != SCAN_MASKED && (MODE & SCAN_LINES) == 0 && (MODE & SCAN_CML) == 0) {
+        if (ee && !((mdn >> k) & 1ull) && lane < (int)min((int64_t)64, ve - vb)) col0 = a.gcol[vb + lane];
+      }
       if (ee) {
         if (sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
         want = early_exit_target<W, LDS_OF(MODE), ALIVE>(a, v, L, g, lw, sv_slot, L.mi[k]);
@@ -1390,9 +1402,9 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
       } else if constexpr ((MODE & 3) == SCAN_PRE) {
         const uint32_t np = L.np[k];
         if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
-        else gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
+        else gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want, col0);
       } else {
-        gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want);
+        gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want, col0);
       }
       reduce_slots<W>(acc);
       if constexpr (ALIVE) {   // the round's gather covered every alive message v lacked: sated
