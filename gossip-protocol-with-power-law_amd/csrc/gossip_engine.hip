@@ -683,7 +683,7 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
       uint8_t lv = 0;
       int32_t u = -1;
       if (lane < n) {
-        u = a.gcol[j0 + lane];
+        u = (col0 != INT32_MIN && j0 == b) ? col0 : a.gcol[j0 + lane];
         lv = lm_of(a.lm, u);
       }
       const u64 ml = __ballot(lv != 0);
@@ -1389,6 +1389,21 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
       if constexpr (GP_COL_EARLY && (MODE & 3) != SCAN_MASKED && (MODE & SCAN_LINES) == 0 && (MODE & SCAN_CML) == 0) {
         if (ee && !((mdn >> k) & 1ull) && lane < (int)min((int64_t)64, ve - vb)) col0 = a.gcol[vb + lane];
       }
+      // line-mask rounds (no early exit): the seen row comes up front too, beside
+      // the first column ids, parked in LDS for the commit (one round trip less)
+#ifndef GP_LINES_SEEN_EARLY
+#define GP_LINES_SEEN_EARLY 1
+#endif
+      constexpr bool SEEN_EARLY = GP_LINES_SEEN_EARLY && W == 64 && (MODE & SCAN_LINES) != 0;
+      if constexpr (SEEN_EARLY) {
+        if (lane < (int)min((int64_t)64, ve - vb)) col0 = a.gcol[vb + lane];
+        const u64x2 sv = load_seen<W>(a, v, sv_slot, lw);
+        if (g == 0) {
+          L.seen[2 * lw] = sv.x;
+          L.seen[2 * lw + 1] = sv.y;
+        }
+        if (sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
+      }
       if (ee) {
         if (sv_slot != SLOT_NONE) st.add(S_SEEN_READ, 1);
         want = early_exit_target<W, LDS_OF(MODE), ALIVE>(a, v, L, g, lw, sv_slot, L.mi[k]);
@@ -1423,7 +1438,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
           wave_sync_lds();
         }
       }
-      finish_row<W, true, (MODE & SCAN_CML) != 0>(a, v, i, acc, lane, g, lw, st, L, ee, sv_slot, k);
+      finish_row<W, true, (MODE & SCAN_CML) != 0>(a, v, i, acc, lane, g, lw, st, L, ee || SEEN_EARLY, sv_slot, k);
     }
     alive_flush<W>(a, L.alive, lane);
     commit_vertices(a, L, li, need, st);
