@@ -535,8 +535,13 @@ __device__ __forceinline__ bool gather_rows(const ExpandArgs& a, const int32_t* 
 #ifndef GP_NEAR_DONE_RIF
 #define GP_NEAR_DONE_RIF 2
 #endif
-  if (RowsInFlight<W>::value > GP_NEAR_DONE_RIF && a.near_done)
-    return gather_rows_n<W, GP_NEAR_DONE_RIF>(a, idx, cnt, g, lw, acc, st, ee, want);
+// (64-word rows already keep 3 in flight; 2 there cost round 4 0.2 ms, r03_ab_nd_lr.txt)
+#ifndef GP_NEAR_DONE_RIF_64
+#define GP_NEAR_DONE_RIF_64 3
+#endif
+  constexpr int ND = W >= 64 ? GP_NEAR_DONE_RIF_64 : GP_NEAR_DONE_RIF;
+  if (RowsInFlight<W>::value > ND && a.near_done)
+    return gather_rows_n<W, ND>(a, idx, cnt, g, lw, acc, st, ee, want);
   return gather_rows_n<W, RowsInFlight<W>::value>(a, idx, cnt, g, lw, acc, st, ee, want);
 }
 
