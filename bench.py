@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--prefilter-pct", type=int, default=20)
     ap.add_argument("--summary-min-n", type=int, default=1 << 25,
                     help="sparse probe rounds of overlays with >= this many vertices read the summary level first")
+    ap.add_argument("--split-deg", type=int, default=128,
+                    help="degree-split sparse rounds: senders of in-degree < this push, receivers probe the "
+                         "gather-order prefix of the others (0 = off; DESIGN.md §3.2)")
     ap.add_argument("--flat-max-words", type=int, default=16,
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--message-order", choices=("given", "spread"), default="spread",
@@ -72,7 +75,7 @@ def parse():
                          "the boundary vertices' new words)")
     ap.add_argument("--profile-steps", action="store_true",
                     help="print per-round stats of the last step to stderr")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     c5 = a.workload == "c5"
     if a.log2n is None:
         a.log2n = 26 if c5 else 24
@@ -106,6 +109,18 @@ def round_bytes(st, words, nloc):
         arcs = 12 * st["arcs_scanned"]
     return (30 * nloc + arcs + st["row_bytes"] + w8 * st["seen_rows_read"]
             + (w8 + 23) * st["rows_written"] + w8 * st.get("lm_rows", 0))
+
+
+def engine_config(args):
+    """The engine configuration of the timed run (tests/test_full_size.py
+    checks a run configured by this very function against the oracle)."""
+    cfg = dict(track_digest=1, track_first=0, hub_threshold=args.hub_threshold, push_ratio=args.push_ratio,
+               early_exit=args.early_exit, unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words,
+               arc_mask_permille=args.arc_mask_permille, compact_rows=args.compact_rows,
+               prefilter_pct=args.prefilter_pct, summary_min_n=args.summary_min_n, split_deg=args.split_deg)
+    if args.workload == "c5":   # SURVEY.md §8d C5: Bernoulli crashes of live vertices, stream seeded by the run seed
+        cfg.update(churn=1, p_fail=args.p_fail, churn_seed=args.seed, miss_threshold=3)
+    return cfg
 
 
 PMC_TRAFFIC = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json")))
@@ -221,15 +236,8 @@ def main():
     n = 1 << args.log2n
     # one GPU per rank; on a smaller box (rehearsal) ranks share devices round-robin
     device = local % max(pkg._lib.device_count(), 1)
-    eng = pkg.GossipEngine(device, track_digest=1, track_first=0, hub_threshold=args.hub_threshold,
-                           push_ratio=args.push_ratio,
-                           early_exit=args.early_exit,
-                           unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words,
-                           arc_mask_permille=args.arc_mask_permille, compact_rows=args.compact_rows,
-                           prefilter_pct=args.prefilter_pct, summary_min_n=args.summary_min_n)
+    eng = pkg.GossipEngine(device, **engine_config(args))
     churn = args.workload == "c5"
-    if churn:   # Bernoulli crashes of live vertices, stream seeded by the run seed
-        eng.configure(churn=1, p_fail=args.p_fail, churn_seed=args.seed, miss_threshold=3)
     t0 = time.perf_counter()
     eng.build_chung_lu(n, args.dbar, args.gamma, args.seed)
     _, nnz, _, _ = eng.info()

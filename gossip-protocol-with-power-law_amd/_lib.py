@@ -89,7 +89,7 @@ class Config(ctypes.Structure):
         ("flat_max_words", ctypes.c_int32),
         ("summary_min_n", ctypes.c_int64),
         ("partition_by_arcs", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("split_deg", ctypes.c_int32),
     ]
 
 
@@ -129,7 +129,7 @@ SIGNATURES = {
     "gp_checkpoint_load": (ctypes.c_int, [_P, _P, _I64]),
 }
 
-ABI_VERSION = 15   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 16   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

@@ -32,6 +32,34 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+STANDIN_SRC = os.path.join(os.path.dirname(PKG_DIR), "tests", "native", "rccl_standin.cpp")
+STANDIN_LIB = os.path.join(OUT_DIR, "libgossip_hip_rccl_standin.so")
+
+
+def build_standin(force=False, verbose=True):
+    """TEST build: the engine's own objects linked against the in-process RCCL
+    stand-in of tests/native/rccl_standin.cpp instead of librccl, so the vertex
+    partition's RCCL path (exchange_rccl) runs with P > 1 ranks as threads of
+    one process on one GPU (tests/test_rccl_standin.py).  The product library
+    (libgossip_hip.so) is not touched."""
+    build(force=force, verbose=verbose)
+    objs = [os.path.join(OUT_DIR, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+    if not force and not _stale(STANDIN_LIB, objs + [STANDIN_SRC, __file__]):
+        return STANDIN_LIB
+    sobj = os.path.join(OUT_DIR, "rccl_standin.o")
+    cmd = [_hipcc(), "-O2", "-std=c++17", "-fPIC", "-Wall", "-c", STANDIN_SRC, "-o", sobj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    tmp = STANDIN_LIB + ".tmp"
+    cmd = [_hipcc(), *FLAGS, "-shared", *objs, sobj, "-o", tmp, "-pthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(tmp, STANDIN_LIB)
+    return STANDIN_LIB
+
+
 def build(force=False, verbose=True):
     os.makedirs(OUT_DIR, exist_ok=True)
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [INCLUDE, __file__]
@@ -59,3 +87,4 @@ def build(force=False, verbose=True):
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_standin(force="--force" in sys.argv)

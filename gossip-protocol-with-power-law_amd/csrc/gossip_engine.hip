@@ -183,11 +183,15 @@ struct ExpandArgs {
   int32_t early_exit;                  // this round scans with the coverage check
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
   int32_t near_done;                   // early-exit round with most messages held: fewer rows in flight
-  int32_t pairs;                       // unfiltered W = 64 round: the SCAN_PAIRS variant (late rounds)
   const u64* __restrict__ alive;       // [W] messages some sender forwards this round (or null)
   int32_t sate;                        // alive early-exit round, no injection left: mark sated receivers
   u64* __restrict__ alive_next;        // [W] the same for round r + 1: OR of the new rows (or null)
   const u64* __restrict__ amask;       // SCAN_MASKED: bit j of word k = sender gcol[64k + j] active
+  const int32_t* __restrict__ prehi;   // degree-split rounds (SCAN_PRE): probe only the first prehi[v]
+                                       //   arcs of v's in-list (senders of in-degree >= split_deg); the
+                                       //   others pushed into acc / tbits before the pull (else null)
+  int32_t split_push;                  // the push half of a degree-split round: no sender / scan counters
+  int32_t acc_row;                     // degree-split rounds: row of `rows` that is row 0 of `acc`
   const uint8_t* __restrict__ lm;      // SCAN_LINES: line mask of each sender's row (0: inactive)
   uint8_t* __restrict__ lm_next;       // W = 64 pulls: the same for round r + 1, written by the commits
                                        //   (nibbles; or null)
@@ -205,7 +209,7 @@ struct ExpandArgs {
   uint32_t* __restrict__ seenpop;
   uint8_t* __restrict__ first;         // may be null
   u64* __restrict__ digest;            // may be null
-  const uint8_t* __restrict__ state;
+  uint8_t* __restrict__ state;         // read by every pull kernel; k_expand's alive variants set ST_SATED
   const int32_t* __restrict__ deg_live;
   u64* __restrict__ partial;
   const HubItem* __restrict__ hub_items;
@@ -295,7 +299,6 @@ template <bool PRE, bool CML>
 struct WaveLdsT {
   static constexpr bool kPre = PRE, kCml = CML;
   u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
-  u64 seen2[64];        // pair paths: the second receiver's seen row
   int32_t idx[64];      // active neighbours of one pass
   uint32_t tot[64];     // k_expand: new bits of the wave's vertex k (committed after the loop)
   uint8_t lmn[64];      // k_expand: line mask of vertex k's new row (committed with tot)
@@ -307,6 +310,7 @@ struct WaveLdsT {
   uint8_t cd[CML ? 64 : 1];       // record-writing rounds: vertex k's row is dense (no record)
   int32_t pre[PRE ? 64 : 1][PRE_IDS];   // SCAN_PRE: active neighbours of vertex k found by the lane phase
   uint8_t np[PRE ? 64 : 1];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
+  uint32_t len[PRE ? 64 : 1];     // SCAN_PRE: in-arcs vertex k scans (its prefix in degree-split rounds)
   u64 alive[64];                  // OR of the new rows this wave wrote (alive_next)
 };
 using WaveLds = WaveLdsT<false, false>;
@@ -406,8 +410,6 @@ enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PR
                 SCAN_CML = 4 /* flag: read / write compact Message-Lists (W = 64) */,
                 SCAN_ALIVE = 8 /* flag: early-exit targets narrowed to the alive messages (k_expand);
                                   a variant of its own: +2-3 VGPRs cost a wave per SIMD */,
-                SCAN_PAIRS = 16 /* flag: receivers with short in-lists two at a time (short_pairs,
-                                   W = 64), a variant of its own for the late latency-bound rounds */,
                 SCAN_LINES = 32 /* flag (W = 64, filtered): the probe reads the sender's line mask
                                    (k_mklm) and the gather loads only its nonzero 128-B lines */ };
 
@@ -869,15 +871,11 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
 #ifndef GP_PRE_PAIRS
 #define GP_PRE_PAIRS 1
 #endif
-#ifndef GP_SHORT_PAIRS
-#define GP_SHORT_PAIRS 0
-#endif
 // rows in flight per half-wave in pre_pairs: 2 (70 VGPRs, 7 waves per SIMD)
 // against 4 (78, 6 waves): C4 round 1 3.97 -> 3.78 ms same-box
 #ifndef GP_PAIR_RIF
 #define GP_PAIR_RIF 2
 #endif
-constexpr int SHORT_DEG = 32;   // in-degree up to which a receiver's arcs fit one half-wave pass
 
 // receiver side of a pair: half h holds receiver ks (on: the half has one;
 // kB < 0: half 1 idle) with its gathered OR acc and its seen row sv
@@ -957,7 +955,9 @@ __device__ __forceinline__ u64x2 pair_seen(const ExpandArgs& a, int h, int lw, b
 
 // SCAN_PRE rounds without early exit (round 1 of a C4 run: 7.9 M receivers,
 // about 2 active in-neighbours each, already found by the lane phase)
-template <int W, class LDS>
+// (LINES: line-mask rounds -- the staged entries are (u << 4) | lines and a
+// lane loads its 16-B piece only when its 128-B line is named)
+template <int W, bool LINES, class LDS>
 __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
                                           WaveStats& st) {
   static_assert(W == 64, "half-wave rows");
@@ -979,118 +979,36 @@ __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
     u64x2 acc = {0, 0};
     const uint32_t nmax = max(npA, npB);
+    uint32_t lines = 0;   // LINES: 128-B lines this half loaded (lane lw == 0 of each half counts)
     for (uint32_t q0 = 0; q0 < nmax; q0 += GP_PAIR_RIF) {
       u64x2 r[GP_PAIR_RIF];
 #pragma unroll
       for (int q = 0; q < GP_PAIR_RIF; ++q) {
         r[q] = u64x2{0, 0};
-        if (q0 + q < np) r[q] = load_piece<W>(a.rows, L.pre[ks][q0 + q], lw);
+        if (q0 + q < np) {
+          const int32_t e = L.pre[ks][q0 + q];
+          if constexpr (LINES) {
+            if ((e >> (lw >> 3)) & 1) r[q] = load_piece<W>(a.rows, e >> 4, lw);
+            lines += (uint32_t)__popc((uint32_t)e & 15u);
+          } else {
+            r[q] = load_piece<W>(a.rows, e, lw);
+          }
+        }
       }
 #pragma unroll
       for (int q = 0; q < GP_PAIR_RIF; ++q) acc |= r[q];
     }
     st.add(S_GATHERED, (u64)(npA + npB));
-    st.add(S_ROW_BYTES, (u64)(npA + npB) * (u64)(8 * W));
+    if constexpr (LINES) {
+      const uint32_t lA = (uint32_t)__builtin_amdgcn_readlane((int)lines, 0);
+      const uint32_t lB = kB >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)lines, 32) : 0u;
+      st.add(S_ROW_BYTES, (u64)(lA + lB) * 128ull);
+    } else {
+      st.add(S_ROW_BYTES, (u64)(npA + npB) * (u64)(8 * W));
+    }
     const u64x2 sv = pair_seen<W>(a, h, lw, on, kB, v, sv_slot, acc, st);
     pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, acc, sv, st);
   }
-}
-
-// receivers with at most SHORT_DEG in-arcs, any pull mode but the per-arc
-// mask: each half-wave loads its receiver's column ids in one pass, probes
-// them, stages the active ones in its half of L.idx and gathers them; early
-// exit (target, word skip, stop) runs per half, the seen row stays in
-// registers
-template <int W, int MODE, bool ALIVE, int RIF, class LDS>
-__device__ __forceinline__ void short_pairs_n(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
-                                              WaveStats& st, bool ee) {
-  static_assert(W == 64, "half-wave rows");
-  const int lane = threadIdx.x & 63, h = lane >> 5, lw = lane & 31;
-  while (mp) {
-    const int kA = __ffsll((long long)mp) - 1;
-    mp &= mp - 1;
-    int kB = -1;
-    if (mp) {
-      kB = __ffsll((long long)mp) - 1;
-      mp &= mp - 1;
-    }
-    const bool on = h == 0 || kB >= 0;
-    const int ks = (h && kB >= 0) ? kB : kA;
-    const int64_t i = base + ks;
-    const int v = (int)(a.vbegin + i);
-    const int64_t vb = L.rp[ks];
-    const int deg = on ? (int)(L.rp[ks + 1] - vb) : 0;
-    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
-    u64x2 want = {0, 0};
-    u64* const pseen = h ? L.seen2 : L.seen;   // early exit: this half's seen row, parked for the commit
-    if (ee) {
-      const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
-      const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
-      st.add(S_SEEN_READ, (u64)((sA != SLOT_NONE ? 1 : 0) + (kB >= 0 && sB != SLOT_NONE ? 1 : 0)));
-      u64x2 sv = {0, 0};
-      if (on) {
-        if (sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
-        u64x2 cm = load_piece<W>(a.cmask, L.mi[ks], lw);
-        if (ALIVE && a.alive) cm &= load_piece<W>(a.alive, 0, lw);
-        want = cm & ~sv;
-      }
-      pseen[2 * lw] = sv.x;
-      pseen[2 * lw + 1] = sv.y;
-    }
-    int32_t ent = -1;
-    if (lw < deg) ent = probe<MODE>(a, a.gcol[vb + lw]);
-    if (ALIVE && ee && a.alive) {   // a half holding every alive message of its component scans nothing
-      const u64 wb = __ballot((want.x | want.y) != 0ull);
-      if (((wb >> (32 * h)) & 0xFFFFFFFFull) == 0ull) ent = -1;
-    }
-    const u64 bm = __ballot(ent >= 0);
-    if (ent >= 0) L.idx[32 * h + __popcll(bm & (((1ull << lw) - 1ull) << (32 * h)))] = ent;
-    wave_sync_lds();
-    const int cntA = __popcll(bm & 0xFFFFFFFFull), cntB = __popcll(bm >> 32);
-    const int cnt = h ? cntB : cntA;
-    st.add(S_ARCS, (u64)((uint32_t)__builtin_amdgcn_readlane(deg, 0) + (uint32_t)__builtin_amdgcn_readlane(deg, 32)));
-    u64x2 acc = {0, 0};
-    bool live = true;   // this lane's words still miss messages (word skip)
-    if (GP_WORD_SKIP && ee) live = (want.x | want.y) != 0ull;
-    const int nmax = max(cntA, cntB);
-    for (int k0 = 0; k0 < nmax; k0 += RIF) {
-      u64x2 r[RIF];
-#pragma unroll
-      for (int q = 0; q < RIF; ++q) {
-        r[q] = u64x2{0, 0};
-        if (k0 + q < cnt && live) r[q] = load_piece<W>(a.rows, L.idx[32 * h + k0 + q], lw);
-      }
-#pragma unroll
-      for (int q = 0; q < RIF; ++q) acc |= r[q];
-      uint32_t pieces = 0;
-#pragma unroll
-      for (int q = 0; q < RIF; ++q) pieces += (uint32_t)line_pieces<W>(__ballot(k0 + q < cnt && live));
-      st.add(S_ROW_BYTES, (u64)pieces * (u64)(8 * Geo<W>::WPL));
-      st.add(S_GATHERED, (u64)(min(RIF, max(cntA - k0, 0)) + min(RIF, max(cntB - k0, 0))));
-      if (ee) {
-        const u64x2 miss = want & ~acc;
-        live = (miss.x | miss.y) != 0ull;
-        if (!__any(live)) break;
-      }
-    }
-    wave_sync_lds();   // L.idx is restaged by the next pair
-    u64x2 sv;
-    if (ee) {
-      sv.x = pseen[2 * lw];
-      sv.y = pseen[2 * lw + 1];
-    } else {
-      sv = pair_seen<W>(a, h, lw, on, kB, v, sv_slot, acc, st);
-    }
-    pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, acc, sv, st);
-  }
-}
-template <int W, int MODE, bool ALIVE, class LDS>
-__device__ __forceinline__ void short_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
-                                            WaveStats& st, bool ee) {
-  if (RowsInFlight<W>::value > GP_NEAR_DONE_RIF && a.near_done)
-    short_pairs_n<W, MODE, ALIVE, GP_NEAR_DONE_RIF>(a, L, mp, base, slot_of, st, ee);
-  else
-    short_pairs_n<W, MODE, ALIVE, RowsInFlight<W>::value>(a, L, mp, base, slot_of, st, ee);
 }
 
 // Done in-neighbours (a.dbits rounds: early exit, no liveness,
@@ -1212,14 +1130,24 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
   const int g = lane / LPR, lw = lane % LPR;
   auto& L = s_w[wib];
   constexpr bool ALIVE = (MODE & SCAN_ALIVE) != 0;
-  constexpr bool PAIRS = (MODE & SCAN_PAIRS) != 0;
-  constexpr int SCAN = MODE & ~(SCAN_ALIVE | SCAN_PAIRS);
+  constexpr int SCAN = MODE & ~SCAN_ALIVE;
   WaveStats st;
   ws_zero(st);
   const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
   if (base < a.nloc) {
     const int64_t li = base + lane;
     bool need = false, act = false, dnb = false;
+    // degree-split rounds: receivers the push half touched (bit k = vertex
+    // base + k; one context: local = global ids).  A touched receiver's
+    // accumulator row is one more entry of its staged list: row a.acc_row + v
+    // of this round's slot buffer is row v of a.acc (same stride, host-checked
+    // offset), so the gathers need no second base pointer.  k_acc_clear zeroes
+    // the rows and the bitmap after the pull (no store here to the rows the
+    // gathers read)
+    u64 tw = 0;
+    if constexpr ((MODE & 3) == SCAN_PRE) {
+      if (a.prehi) tw = a.tbits[base >> 6];
+    }
     u64 sends = 0;
     uint32_t slot_of = SLOT_NONE;
     uint32_t pre_arcs = 0;   // SCAN_PRE: arcs the lane phase scanned
@@ -1240,8 +1168,11 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
         // wave's serial loop skips vertices with no active in-neighbour and
         // starts the others at their rows
         uint32_t np = 0xFFu;
-        if (need && e - b <= PRE_MAX_DEG) {
-          const int deg = (int)(e - b);
+        const bool tch = (tw >> lane) & 1ull;
+        const int64_t se = a.prehi ? b + a.prehi[v] : e;   // end of the arcs this vertex scans
+        L.len[lane] = (uint32_t)(se - b);
+        if (need && se - b <= PRE_MAX_DEG) {
+          const int deg = (int)(se - b);
           uint32_t cnt = 0;
 #pragma unroll
           for (int h = 0; h < PRE_MAX_DEG / PRE_IDS; ++h) {
@@ -1250,6 +1181,21 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
               u64 w[PRE_IDS];
 #pragma unroll
               for (int q = 0; q < PRE_IDS; ++q) c[q] = h * PRE_IDS + q < deg ? a.gcol[b + h * PRE_IDS + q] : -1;
+              if constexpr ((MODE & SCAN_LINES) != 0) {
+                // line-mask rounds: the probe reads the sender's nibble (0: not a
+                // sender) and the staged entry carries it, (u << 4) | lines
+                uint32_t lv[PRE_IDS];
+#pragma unroll
+                for (int q = 0; q < PRE_IDS; ++q) lv[q] = c[q] >= 0 ? (uint32_t)lm_of(a.lm, c[q]) : 0u;
+#pragma unroll
+                for (int q = 0; q < PRE_IDS; ++q) {
+                  if (lv[q]) {
+                    if (cnt < (uint32_t)PRE_IDS) L.pre[lane][cnt] = (c[q] << 4) | (int32_t)lv[q];
+                    ++cnt;
+                  }
+                }
+                continue;
+              }
 #if GP_SUMMARY_PROBE
               if (a.sbits) {   // summary level first: L2-resident, most probes end there
                 u64 sw[PRE_IDS];
@@ -1271,7 +1217,8 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
               }
             }
           }
-          if (cnt <= (uint32_t)PRE_IDS) {
+          if (cnt + (tch ? 1u : 0u) <= (uint32_t)PRE_IDS) {
+            if (tch) L.pre[lane][cnt++] = a.acc_row + v;   // the accumulator row: one more entry
             np = cnt;
             pre_arcs = (uint32_t)deg;
           }
@@ -1302,7 +1249,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
       // loads in flight together) instead of one receiver's chain after the
       // other in the serial loop; those with at most PRE_IDS active
       // neighbours join the prefiltered receivers, those with none drop out
-      u64 mw = __ballot(need && L.np[lane] == 0xFFu && L.rp[lane + 1] - L.rp[lane] <= GP_WAVE_PRE_MAX);
+      u64 mw = __ballot(need && L.np[lane] == 0xFFu && L.len[lane] <= GP_WAVE_PRE_MAX);
       u64 zero = 0;   // no active in-neighbour: nothing to scan (commit writes fpop_next = 0)
       uint32_t arcs = 0;
       while (mw) {
@@ -1318,10 +1265,15 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
           c[q] = -1;
           if (kq[q] >= 0) {
             const int64_t b = L.rp[kq[q]];
-            if (lane < (int)(L.rp[kq[q] + 1] - b)) c[q] = a.gcol[b + lane];
+            if (lane < (int)L.len[kq[q]]) c[q] = a.gcol[b + lane];
           }
         }
         u64 w[GP_WAVE_PRE_N];
+        uint32_t lq[GP_WAVE_PRE_N];   // line-mask rounds: the senders' nibbles
+        if constexpr ((MODE & SCAN_LINES) != 0) {
+#pragma unroll
+          for (int q = 0; q < GP_WAVE_PRE_N; ++q) lq[q] = c[q] >= 0 ? (uint32_t)lm_of(a.lm, c[q]) : 0u;
+        } else
 #if GP_SUMMARY_PROBE
         if (a.sbits) {
           u64 sw[GP_WAVE_PRE_N];
@@ -1337,14 +1289,25 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
 #pragma unroll
         for (int q = 0; q < GP_WAVE_PRE_N; ++q) {
           if (kq[q] < 0) continue;
-          const bool act = c[q] >= 0 && ((w[q] >> (c[q] & 63)) & 1ull);
+          bool act;
+          int32_t ent = c[q];
+          if constexpr ((MODE & SCAN_LINES) != 0) {
+            act = lq[q] != 0u;
+            ent = (c[q] << 4) | (int32_t)lq[q];
+          } else {
+            act = c[q] >= 0 && ((w[q] >> (c[q] & 63)) & 1ull);
+          }
           const u64 am = __ballot(act);
-          const int cnt = __popcll(am);
+          const int tq = (int)((tw >> kq[q]) & 1ull);   // degree-split: + the accumulator row
+          const int cnt = __popcll(am) + tq;
           if (cnt <= PRE_IDS) {   // (more: the serial loop scans it, and counts its arcs)
-            if (act) L.pre[kq[q]][lane_rank(am)] = c[q];
-            if (lane == 0) L.np[kq[q]] = (uint8_t)cnt;
+            if (act) L.pre[kq[q]][lane_rank(am)] = ent;
+            if (lane == 0) {
+              if (tq) L.pre[kq[q]][cnt - 1] = a.acc_row + (int32_t)(base + kq[q]);
+              L.np[kq[q]] = (uint8_t)cnt;
+            }
             if (cnt == 0) zero |= 1ull << kq[q];
-            arcs += (uint32_t)(L.rp[kq[q] + 1] - L.rp[kq[q]]);
+            arcs += L.len[kq[q]];
           }
         }
       }
@@ -1356,7 +1319,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
     if constexpr (GP_PRE_PAIRS && W == 64 && (MODE & 3) == SCAN_PRE) {
       if (!ee) {   // prefiltered receivers two at a time, the rest below
         const u64 mp = m & __ballot(need && L.np[lane] != 0xFFu);
-        pre_pairs<W>(a, L, mp, base, slot_of, st);
+        pre_pairs<W, (MODE & SCAN_LINES) != 0>(a, L, mp, base, slot_of, st);
         m &= ~mp;
       }
     }
@@ -1365,15 +1328,6 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
         const u64 md = m & mdn;
         dnb_pairs<W>(a, L, md, base, slot_of, st);
         m &= ~md;
-      }
-    }
-    if constexpr ((GP_SHORT_PAIRS || PAIRS) && W == 64 && (MODE & 3) != SCAN_MASKED) {
-      bool pairs = true;   // (record rounds read records in the single-receiver scan)
-      if constexpr ((MODE & SCAN_CML) != 0) pairs = a.cmk == nullptr;
-      if (pairs) {   // receivers with short in-lists two at a time, the rest below
-        const u64 msp = m & __ballot(need && L.rp[lane + 1] - L.rp[lane] <= SHORT_DEG);
-        short_pairs<W, SCAN, ALIVE>(a, L, msp, base, slot_of, st, ee);
-        m &= ~msp;
       }
     }
     u64 sat = 0;   // receivers of this wave found sated (alive rounds)
@@ -1421,8 +1375,19 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
         acc = want;
       } else if constexpr ((MODE & 3) == SCAN_PRE) {
         const uint32_t np = L.np[k];
-        if (np != 0xFFu) gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
-        else gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want, col0);
+        if (np != 0xFFu) {
+          if constexpr (W == 64 && (MODE & SCAN_LINES) != 0)
+            gather_lines<GP_LINES_RIF>(a, L.pre[k], (int)np, g, lw, acc, st);   // (u << 4) | lines entries
+          else
+            gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
+        } else {
+          gather_scan<W, SCAN>(a, vb, vb + L.len[k], L, lane, g, lw, acc, st, ee, want, col0);
+          if ((tw >> k) & 1ull) {   // degree-split: the accumulator row (not staged: a scanned receiver)
+            if (g == 0) acc |= load_piece<W>(a.acc, v, lw);
+            st.add(S_GATHERED, 1);
+            st.add(S_ROW_BYTES, (u64)(8 * W));
+          }
+        }
       } else {
         gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want, col0);
       }
@@ -1448,7 +1413,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
     alive_flush<W>(a, L.alive, lane);
     commit_vertices(a, L, li, need, st);
     if constexpr (ALIVE) {
-      if (sat && ((sat >> lane) & 1ull)) const_cast<uint8_t*>(a.state)[a.vbegin + li] |= ST_SATED;
+      if (sat && ((sat >> lane) & 1ull)) a.state[a.vbegin + li] |= ST_SATED;
     }
   }
   flush_stats(st, a.partial);
@@ -2070,6 +2035,7 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
       if (g == 0) {
         for (int p = p0; p < p1; ++p)
           if (a.hub_pnz[p]) acc |= load_piece<W>(a.hub_partial, p, lw);
+        if (a.prehi) acc |= load_piece<W>(a.acc, v, lw);   // degree-split round: the push half's OR (k_acc_clear zeroes it)
       }
       finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
     }
@@ -2091,10 +2057,13 @@ __global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
 
 // active senders from the bitmap: one thread per 64-vertex word, block-level
 // compaction, one cursor add per block; big senders go to their own list
+// (split_deg > 0: the push half of a degree-split round lists only senders of
+// in-degree < split_deg; the others are pulled by the receivers' prefix probes)
 __global__ __launch_bounds__(BLOCK) void k_active_list(const u64* __restrict__ abits, int64_t nwords,
                                                        const int64_t* __restrict__ orp, int32_t big_thr,
                                                        int32_t* __restrict__ active, int32_t* __restrict__ big,
-                                                       u64* __restrict__ stats) {
+                                                       u64* __restrict__ stats, const int64_t* __restrict__ rp_in,
+                                                       int32_t split_deg) {
   __shared__ uint32_t s_cnt[BLOCK];
   __shared__ u64 s_base;
   const int64_t w = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -2115,7 +2084,9 @@ __global__ __launch_bounds__(BLOCK) void k_active_list(const u64* __restrict__ a
     const int b = __ffsll((long long)m) - 1;
     m &= m - 1;
     const int32_t u = (int32_t)(w * 64 + b);
-    if (orp[u + 1] - orp[u] > big_thr) {
+    if (split_deg > 0 && rp_in[u + 1] - rp_in[u] >= split_deg) {
+      active[pos++] = -1;   // pulled (placeholder: the block's slots stay dense)
+    } else if (orp[u + 1] - orp[u] > big_thr) {
       const u64 k = atomicAdd(&stats[S_BIG_CURSOR], 1ull);
       big[k] = u;
       active[pos++] = -1;   // placeholder keeps the block's slots dense
@@ -2193,6 +2164,7 @@ __device__ __forceinline__ int stage_row(const ExpandArgs& a, int32_t u, u64* __
 }
 
 __device__ __forceinline__ void push_sender_stats(const ExpandArgs& a, int32_t u, WaveStats& st) {
+  if (a.split_push) return;   // (the pull half of a degree-split round counts every sender)
   if (u >= a.vbegin && u < a.vbegin + a.nloc) {
     st.add(S_SENDS, (u64)a.fpop[u] * (u64)(uint32_t)max(a.deg_live[u], 0));
     st.add(S_ACTIVE, 1);
@@ -2215,9 +2187,11 @@ __global__ __launch_bounds__(BLOCK) void k_push(ExpandArgs a) {
     push_sender_stats(a, u, st);
     const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
     const int64_t jb = a.orp[u], je = a.orp[u + 1];
-    st.add(S_GATHERED, 1);
-    st.add(S_ROW_BYTES, (u64)(8 * W));
-    st.add(S_ARCS, (u64)(je - jb));
+    if (!a.split_push) {
+      st.add(S_GATHERED, 1);
+      st.add(S_ROW_BYTES, (u64)(8 * W));
+      st.add(S_ARCS, (u64)(je - jb));
+    }
     st.add(S_ATOMICS, (u64)(je - jb) * (u64)nnz);
     push_arcs<W>(a, jb, je, s_row[wib], s_words[wib], nnz, lane);
     __builtin_amdgcn_wave_barrier();
@@ -2244,7 +2218,7 @@ __global__ __launch_bounds__(BLOCK) void k_push_big(ExpandArgs a) {
     const int64_t jb = a.orp[u], je = a.orp[u + 1];
     const int64_t nch = (je - jb + PUSH_CHUNK - 1) / PUSH_CHUNK;
     const int64_t c0 = ((gw - (k * 7919) % nw) % nw + nw) % nw;   // first chunk of this wave
-    if (c0 == 0 && gw == (k * 7919) % nw) {
+    if (c0 == 0 && gw == (k * 7919) % nw && !a.split_push) {
       push_sender_stats(a, u, st);
       st.add(S_GATHERED, 1);
       st.add(S_ROW_BYTES, (u64)(8 * W));
@@ -2253,13 +2227,31 @@ __global__ __launch_bounds__(BLOCK) void k_push_big(ExpandArgs a) {
     const int nnz = stage_row<W>(a, u, s_row[wib], s_words[wib], lane);
     for (int64_t c = c0; c < nch; c += nw) {
       const int64_t cb = jb + c * PUSH_CHUNK, ce = min(je, cb + PUSH_CHUNK);
-      st.add(S_ARCS, (u64)(ce - cb));
+      if (!a.split_push) st.add(S_ARCS, (u64)(ce - cb));
       st.add(S_ATOMICS, (u64)(ce - cb) * (u64)nnz);
       push_arcs<W>(a, cb, ce, s_row[wib], s_words[wib], nnz, lane);
     }
     __builtin_amdgcn_wave_barrier();
   }
   flush_stats(st, a.partial);
+}
+
+// degree-split rounds, after the pull: zero the accumulator rows the push half
+// wrote (every touched receiver's; the pull only read them) and the bitmap
+template <int W>
+__global__ __launch_bounds__(BLOCK) void k_acc_clear(u64* __restrict__ tbits, u64* __restrict__ acc, int64_t nwords) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * WAVES;
+  for (int64_t w = (int64_t)blockIdx.x * WAVES + uniform(threadIdx.x >> 6); w < nwords; w += nw) {
+    u64 bits = tbits[w];
+    if (!bits) continue;
+    while (bits) {
+      const int b = __ffsll((long long)bits) - 1;
+      bits &= bits - 1;
+      if (lane < W) acc[(size_t)(w * 64 + b) * W + lane] = 0ull;
+    }
+    if (lane == 0) tbits[w] = 0ull;
+  }
 }
 
 // receiver side of the push: one wave per touched vertex
@@ -2350,8 +2342,8 @@ __global__ __launch_bounds__(BLOCK) void k_apply_lanes(ExpandArgs a) {
       const bool rn = base + r < nt;
       u64x2 acc = {0, 0};
       if (rn) {
-        acc = load_piece<W>(a.acc, rv - a.vbegin, lw);
-        store_piece<W>(a.acc, rv - a.vbegin, lw, u64x2{0, 0});   // the accumulator stays all-zero
+        acc = load_piece<W>(a.acc, rv, lw);   // (indexed by v, as push_arcs and k_apply do)
+        store_piece<W>(a.acc, rv, lw, u64x2{0, 0});   // the accumulator stays all-zero
       }
       const bool any = group_or<LPR>((acc.x | acc.y) != 0ull);
       u64x2 sv = {0, 0};
@@ -3417,6 +3409,9 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.sbits = c->sum_now ? c->d_sbits : nullptr;
   a.dbits = c->dnb_now ? c->d_dbits : nullptr;
   a.amask = c->d_amask;
+  a.prehi = c->split_now ? c->d_prehi : nullptr;
+  a.split_push = 0;
+  a.acc_row = c->split_now ? c->acc_row : 0;
   a.lm = c->lines_now ? (c->lm_written_prev && !alive_on(c) ? c->d_lmw[c->cur] : c->d_lm) : nullptr;
   a.lm_next = c->lm_write_now ? c->d_lmw[c->cur ^ 1] : nullptr;
   a.cmk = c->cml_read_now ? c->d_cmk[c->cur] : nullptr;
@@ -3478,7 +3473,7 @@ static void launch_push_w(Ctx* c, ExpandArgs a) {
     a.nbits = c->d_nbits;
   }
   hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_abits, nwords,
-                     a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats);
+                     a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats, (const int64_t*)nullptr, 0);
   hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_touch_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_tbits, nwords,
@@ -3535,10 +3530,27 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
                          c->d_gcol, c->d_abits, c->d_amask, kb, c->nnz_l);
   }
   const int mode = a.unfiltered ? SCAN_UNFILTERED : SCAN_FILTERED;
+  if (a.prehi) {   // degree-split round, push half: senders of in-degree < split_deg
+    ExpandArgs p = a;
+    p.split_push = 1;
+    const int64_t nwords = (c->n_alloc + 63) / 64;
+    hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, c->stream, c->d_abits, nwords,
+                       a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats, (const int64_t*)c->d_row_ptr,
+                       c->cfg.split_deg);
+    hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, c->stream, p);
+    hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, c->stream, p);
+  }
   (void)hipEventRecord(c->ev[4], c->stream);
   // line masks of the senders' rows (SCAN_LINES; inside the pull's events and bytes)
   const bool lines = W == 64 && a.lm != nullptr && !flat && !masked && mode == SCAN_FILTERED && !a.cmk &&
                      !a.cmk_next && !c->prefilter_now && !(a.alive && a.early_exit);
+  // line-mask rounds probe the in-lists of low-degree receivers in the lane
+  // phase (the prefilter's machinery, all probes of the wave in flight at once)
+  // and gather them two receivers at a time: the per-receiver chain of column
+  // ids -> probes -> rows is the bound of these rounds
+#ifndef GP_LINES_PRE
+#define GP_LINES_PRE 0
+#endif
   if (lines && a.lm == c->d_lm)   // (the last round's commits did not write them)
     hipLaunchKernelGGL(k_mklm, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
                        dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], a.rows, c->n_alloc, c->d_lm, a.partial);
@@ -3562,12 +3574,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
       if constexpr (W >= 32)
         hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
     } else if (mode == SCAN_UNFILTERED) {
-      bool pairs = false;   // late near-done rounds: short in-lists two receivers at a time
-      if constexpr (W == 64) pairs = a.pairs != 0;
-      if constexpr (W == 64) {
-        if (pairs) hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_PAIRS>), grid, dim3(BLOCK), 0, c->stream, a);
-      }
-      if (!pairs) hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+      hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
     }
     else if (masked)
       hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(BLOCK), 0, c->stream, a);
@@ -3596,8 +3603,15 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
         }
       }
       if constexpr (W == 64) {
-        if (!done && lines) {
+        if (!done && lines && GP_LINES_PRE) {   // low-degree receivers probed lane-parallel
+          hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_LINES>), grid, dim3(BLOCK), 0, c->stream, a);
+          c->lines_ran = true;
+          c->lines_from_commits = a.lm != c->d_lm;
+          done = true;
+        } else if (!done && lines) {
           hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_LINES>), grid, dim3(BLOCK), 0, c->stream, a);
+          c->lines_ran = true;
+          c->lines_from_commits = a.lm != c->d_lm;
           done = true;
         }
       }
@@ -3622,6 +3636,11 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   // kernel_ms brackets the pull kernel and the hub passes: the round's
   // counters (row bytes, arcs scanned, rows written) include the hubs' share
   (void)hipEventRecord(c->ev[5], c->stream);
+  if (a.prehi) {   // degree-split round: the accumulator back to all-zero
+    const int64_t nwords = (c->n_alloc + 63) / 64;
+    hipLaunchKernelGGL(k_acc_clear<W>, dim3(std::max(1, std::min(grid_for(nwords, WAVES), c->cu_count * 8))),
+                       dim3(BLOCK), 0, c->stream, c->d_tbits, c->d_acc, nwords);
+  }
 }
 
 #ifndef GP_PARK
@@ -3750,6 +3769,22 @@ static int launch_expand(Ctx* c) {
   // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
   c->prefilter_now = !c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.prefilter_pct > 0 &&
                      senders * 100.0 < (double)c->cfg.prefilter_pct * (double)c->n;
+  // degree-split: a prefiltered per-receiver pull without
+  // early exit (C4 / C5 round 1), one context, no compact Message-Lists:
+  // senders of in-degree < split_deg push (few arcs: they are the
+  // low-degree minority of a degree-biased sender set), receivers probe only
+  // the gather-order prefix of bigger senders
+  c->split_now = c->cfg.split_deg > 0 && c->prefilter_now && !c->early_exit_now && !c->local &&
+                 c->nloc() == c->n_alloc && !c->cml_read_now && !c->cml_write_now &&
+                 !(c->words <= 32 && c->words <= c->cfg.flat_max_words);
+  if (c->split_now) {   // accumulator rows as rows of this round's slot buffer (same stride)
+    const ptrdiff_t d = reinterpret_cast<const char*>(c->d_acc) - reinterpret_cast<const char*>(c->d_slot[c->cur]);
+    const ptrdiff_t rb = (ptrdiff_t)c->words * 8;
+    const int64_t row = d / rb;
+    c->split_now = d % rb == 0 && row >= (int64_t)INT32_MIN && row + c->n_alloc <= (int64_t)INT32_MAX;
+    c->acc_row = (int32_t)row;
+  }
+  if (c->split_now) GP_TRY(build_prehi(c, c->cfg.split_deg));
   ExpandArgs a{};
   fill_expand(c, a);
   a.unfiltered = c->unfiltered_now ? 1 : 0;
@@ -3758,19 +3793,13 @@ static int launch_expand(Ctx* c) {
   // C5 rounds 5-6 56.8 -> 64.3 ms with the switch on)
   a.near_done = c->early_exit_now && !c->liveness_active &&
                 (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m ? 1 : 0;
-  // paired short in-lists in the late near-done rounds (few new bits last
-  // round: receivers complete after a few rows, the serial chain is the bound)
-#ifndef GP_PAIRS_DIV
-#define GP_PAIRS_DIV 0.0   // SCAN_PAIRS when last round's new bits <= n*m / GP_PAIRS_DIV (0: never)
-#endif
-  a.pairs = GP_PAIRS_DIV > 0.0 && a.near_done && a.unfiltered &&
-            (double)c->prev_new_bits * GP_PAIRS_DIV <= (double)c->n * (double)c->m ? 1 : 0;
   // sated vertices (churn): with no injection left, a receiver that ends the
   // round holding every alive message of its component never receives again
 #ifndef GP_SATE
 #define GP_SATE 1
 #endif
   a.sate = GP_SATE && alive_on(c) && c->early_exit_now && c->round >= c->last_inject_round ? 1 : 0;
+  c->lines_ran = c->lines_from_commits = false;
   switch (c->words) {
     case 1: launch_expand_w<1>(c, a); break;
     case 2: launch_expand_w<2>(c, a); break;
@@ -3943,6 +3972,8 @@ int finish_graph(Ctx* c) {
   GP_TRY(dalloc(&c->d_comp, (size_t)c->n));
   GP_TRY(components(c));
   GP_TRY(build_gather_order(c));
+  dfree(&c->d_prehi);   // (degree-split prefixes: rebuilt on first use for this overlay)
+  c->prehi_deg = 0;
   c->h_deg_out.resize((size_t)c->n);
   GP_HIP(hipMemcpyAsync(c->h_deg_out.data(), c->d_deg_out, (size_t)c->n * 4, hipMemcpyDeviceToHost, c->stream));
   c->h_row_ptr.resize((size_t)c->n + 1);
@@ -4146,6 +4177,7 @@ void gp_default_config(gp_config* cfg) {
   cfg->flat_max_words = 16;
   cfg->summary_min_n = 1ll << 25;   // activity bitmap > 4 MB: outgrows an XCD's L2
   cfg->partition_by_arcs = 0;       // vertex partitions: equal vertex counts (1: equal arc counts)
+  cfg->split_deg = 128;             // degree-split sparse rounds
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -4184,7 +4216,7 @@ void gp_destroy(gp_ctx* c) {
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
   dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_lmw[0]); dfree(&c->d_lmw[1]); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
-  dfree(&c->d_gcol); dfree(&c->d_midx); dfree(&c->d_cmask);
+  dfree(&c->d_gcol); dfree(&c->d_prehi); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_inj_origin); dfree(&c->d_inj_bits); dfree(&c->d_inj_cnt);
   dfree(&c->d_slot[2]);
@@ -4216,6 +4248,7 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->arc_mask_permille < 0) return set_error(GP_EINVAL, "arc_mask_permille < 0");
   if (cfg->partition_by_arcs != 0 && cfg->partition_by_arcs != 1)
     return set_error(GP_EINVAL, "partition_by_arcs must be 0 or 1");
+  if (cfg->split_deg < 0) return set_error(GP_EINVAL, "split_deg must be >= 0");
   if (c->local && cfg->partition_by_arcs != c->cfg.partition_by_arcs)
     return set_error(GP_ESTATE, "a partitioned context keeps its partition: reload the overlay to change it");
   GP_HIP(hipSetDevice(c->device));
@@ -4412,9 +4445,12 @@ int gp_spread_keys(gp_ctx* c, int32_t hops, int32_t m, const int32_t* origin, ui
   } else {
     int32_t* d_o = nullptr;
     u64 *d_k = nullptr, *d_s2 = nullptr;
-    GP_HIP(hipMalloc(&d_o, (size_t)m * sizeof(int32_t)));
-    GP_HIP(hipMalloc(&d_k, (size_t)m * sizeof(u64)));
-    int rc = copy_sync(c, d_o, origin, (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice);
+    // every allocation goes through rc, so the frees below always run
+    int rc = 0;
+    if (hipMalloc(&d_o, (size_t)m * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&d_k, (size_t)m * sizeof(u64)) != hipSuccess)
+      rc = set_error(GP_ENOMEM, "gp_spread_keys: message scratch");
+    if (rc == 0) rc = copy_sync(c, d_o, origin, (size_t)m * sizeof(int32_t), hipMemcpyHostToDevice);
     if (rc == 0 && hops == 3 && hipMalloc(&d_s2, (size_t)c->n * sizeof(u64)) != hipSuccess)
       rc = set_error(GP_ENOMEM, "gp_spread_keys: n u64 of scratch");
     if (rc == 0) {
@@ -4426,10 +4462,10 @@ int gp_spread_keys(gp_ctx* c, int32_t hops, int32_t m, const int32_t* origin, ui
       hipLaunchKernelGGL(k_nbsum, dim3(std::min(grid_for(m, BLOCK / 64), 65536)), dim3(BLOCK), 0, c->stream,
                          c->d_row_ptr, c->d_col, (const u64*)d_s2, (const int32_t*)d_o, (int64_t)m, d_k);
       if (hipGetLastError() != hipSuccess) rc = set_error(GP_EHIP, "gp_spread_keys: launch failed");
-      rc = copy_sync(c, keys.data(), d_k, (size_t)m * sizeof(u64), hipMemcpyDeviceToHost);
+      if (rc == 0) rc = copy_sync(c, keys.data(), d_k, (size_t)m * sizeof(u64), hipMemcpyDeviceToHost);
     }
-    (void)hipFree(d_o);
-    (void)hipFree(d_k);
+    if (d_o) (void)hipFree(d_o);
+    if (d_k) (void)hipFree(d_k);
     if (d_s2) (void)hipFree(d_s2);
     if (rc) return rc;
   }
@@ -4678,7 +4714,8 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->row_bytes = h[S_ROW_BYTES];
     out->mode = c->mode_push ? 1 : 0;
     out->scan = c->mode_push ? 0 : (c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : c->prefilter_now ? 3 : 0) |
-                                       (c->cml_read_now ? 4 : 0);
+                                       (c->cml_read_now ? 4 : 0) | (c->lines_ran ? 8 : 0) |
+                                       (c->lines_from_commits ? 16 : 0) | (c->split_now ? 32 : 0);
     out->kernel_ms = 0.0;
     if (!c->mode_push && c->nloc() > 0) {
       float kms = 0.f;
@@ -4840,18 +4877,26 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(nl * W * 8));
       if (bytes) {   // owned rows of every slot, picked per vertex by its slot byte
-        std::vector<uint64_t> s1((size_t)(nl * W)), s2(c->d_slot[2] ? (size_t)(nl * W) : 0);
+        // blocks of rows: host scratch stays at 2 blocks whatever n (a 2^26 x
+        // 4096 read would otherwise hold two more 32 GiB copies)
+        const int64_t blk = std::max<int64_t>(1, (int64_t(64) << 20) / (W * 8));
+        std::vector<uint64_t> s1((size_t)(std::min(nl, blk) * W)), s2(c->d_slot[2] ? s1.size() : 0);
         std::vector<uint8_t> sp((size_t)nl);
-        GP_TRY(copy_sync(c, host, c->d_slot[0], (size_t)bytes, hipMemcpyDeviceToHost));
-        GP_TRY(copy_sync(c, s1.data(), c->d_slot[1], (size_t)bytes, hipMemcpyDeviceToHost));
-        if (c->d_slot[2]) GP_TRY(copy_sync(c, s2.data(), c->d_slot[2], (size_t)bytes, hipMemcpyDeviceToHost));
         GP_TRY(copy_sync(c, sp.data(), c->d_sp, (size_t)nl, hipMemcpyDeviceToHost));
         uint64_t* h = static_cast<uint64_t*>(host);
-        for (int64_t v = 0; v < nl; ++v) {
-          const uint8_t p = sp[(size_t)v];
-          if (p == SLOT_NONE) std::memset(h + v * W, 0, (size_t)W * 8);
-          else if (p == 1) std::memcpy(h + v * W, s1.data() + v * W, (size_t)W * 8);
-          else if (p == SLOT_PARKED && !s2.empty()) std::memcpy(h + v * W, s2.data() + v * W, (size_t)W * 8);
+        for (int64_t v0 = 0; v0 < nl; v0 += blk) {
+          const int64_t k = std::min(blk, nl - v0);
+          const size_t kb = (size_t)(k * W * 8);
+          GP_TRY(copy_sync(c, h + v0 * W, c->d_slot[0] + v0 * W, kb, hipMemcpyDeviceToHost));
+          GP_TRY(copy_sync(c, s1.data(), c->d_slot[1] + v0 * W, kb, hipMemcpyDeviceToHost));
+          if (c->d_slot[2]) GP_TRY(copy_sync(c, s2.data(), c->d_slot[2] + v0 * W, kb, hipMemcpyDeviceToHost));
+          for (int64_t v = v0; v < v0 + k; ++v) {
+            const uint8_t p = sp[(size_t)v];
+            const int64_t o = (v - v0) * W;
+            if (p == SLOT_NONE) std::memset(h + v * W, 0, (size_t)W * 8);
+            else if (p == 1) std::memcpy(h + v * W, s1.data() + o, (size_t)W * 8);
+            else if (p == SLOT_PARKED && !s2.empty()) std::memcpy(h + v * W, s2.data() + o, (size_t)W * 8);
+          }
         }
       }
       return 0;

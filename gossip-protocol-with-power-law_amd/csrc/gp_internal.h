@@ -160,6 +160,11 @@ struct Ctx {
   // without k_mklm's pass over the senders' rows
   uint8_t* d_lmw[2] = {nullptr, nullptr};
   bool lm_write_now = false, lm_written_prev = false;
+  // what this round's pull actually ran (round stats' scan bits 8 / 16): the
+  // line-mask variant, and with masks the previous round's commits wrote
+  bool lines_ran = false, lines_from_commits = false;
+  bool split_now = false;   // degree-split round: low-degree senders push, receivers probe a prefix
+  int32_t acc_row = 0;      // its accumulator rows addressed as rows of the round's slot buffer
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
   u64* d_amask = nullptr;
   // push (sparse-round) mode
@@ -188,6 +193,9 @@ struct Ctx {
     return it == inject.end() ? 0 : it->second.cnt;
   }
   int32_t* d_gcol = nullptr;        // [nnz] in-CSR columns, rows sorted by neighbour degree desc
+  int32_t* d_prehi = nullptr;       // [n] degree-split rounds: gather-order prefix of senders with
+                                    //   in-degree >= prehi_deg (build_prehi, built on first use)
+  int32_t prehi_deg = 0;
   int32_t* d_midx = nullptr;        // [n_alloc] component mask row of v (-1: none)
   u64* d_cmask = nullptr;           // [K][W] messages per component
   std::vector<int32_t> h_inj_origin;   // host copies of the injection groups
@@ -285,6 +293,7 @@ int copy_sync(Ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind ki
 // graph_build.hip
 int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed);
 int build_gather_order(Ctx* c);
+int build_prehi(Ctx* c, int32_t T);
 // gossip_engine.hip
 int finish_graph(Ctx* c);
 int build_hubs(Ctx* c);

@@ -269,4 +269,34 @@ int build_gather_order(Ctx* c) {
   return 0;
 }
 
+// degree-split rounds: per vertex, the length of the prefix
+// of its gather-ordered in-list whose senders have in-degree >= T (the order is
+// by that in-degree, descending, so the prefix is exactly those arcs).  One
+// thread per vertex, binary search over its segment.
+__global__ void k_prehi(const int64_t* __restrict__ rp, const int32_t* __restrict__ gcol, int64_t n, int32_t T,
+                        int32_t* __restrict__ prehi) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= n) return;
+  int64_t lo = rp[v], hi = rp[v + 1];   // first j in [lo, hi) with deg(gcol[j]) < T
+  const int64_t b = lo;
+  while (lo < hi) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    const int32_t u = gcol[mid];
+    if (rp[u + 1] - rp[u] >= (int64_t)T) lo = mid + 1;
+    else hi = mid;
+  }
+  prehi[v] = (int32_t)(lo - b);
+}
+
+int build_prehi(Ctx* c, int32_t T) {
+  if (c->d_prehi && c->prehi_deg == T) return 0;
+  GP_TRY(dalloc(&c->d_prehi, (size_t)std::max<int64_t>(c->n, 1)));
+  if (c->n > 0)
+    hipLaunchKernelGGL(k_prehi, dim3((unsigned)((c->n + 255) / 256)), dim3(256), 0, c->stream, c->d_row_ptr,
+                       c->d_gcol, c->n, T, c->d_prehi);
+  GP_HIP(hipGetLastError());
+  c->prehi_deg = T;
+  return 0;
+}
+
 }  // namespace gp

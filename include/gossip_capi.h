@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 15
+#define GP_ABI_VERSION 16
 
 typedef struct gp_ctx gp_ctx;
 
@@ -85,7 +85,10 @@ typedef struct gp_round_stats {
                                bitmap probe per arc, 1 = per-arc activity mask built
                                first, 2 = none, every in-neighbour row read (§3.4),
                                3 = probe, low-degree in-lists prefiltered (§3.2);
-                               + 4: senders gathered from compact Message-Lists     */
+                               + 4: senders gathered from compact Message-Lists;
+                               + 8: 64-word line masks read (only named 128-B lines
+                               gathered, §3.2); + 16: those masks were written by
+                               the previous round's commits (no k_mklm pass)       */
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
@@ -141,7 +144,12 @@ typedef struct gp_config {
   int32_t partition_by_arcs;   /* vertex partitions (gp_set_partition): 0 = slices of equal
                                   vertex count, 1 = slices of equal in-arc count
                                   (set before the partition is made)     */
-  int32_t reserved0;           /* zero                                                   */
+  int32_t split_deg;           /* degree-split sparse rounds: in a
+                                  prefiltered pull without early exit, senders of
+                                  in-degree < split_deg push their rows (atomicOr into
+                                  the accumulator) and receivers probe only the prefix of
+                                  their gather-ordered in-list whose senders have
+                                  in-degree >= split_deg (0 = off; single-rank contexts) */
 } gp_config;
 
 /* what for gp_read */

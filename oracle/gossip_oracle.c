@@ -25,6 +25,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -186,7 +187,11 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
   while (W * 64 < m) W <<= 1;
   uint64_t* front = (uint64_t*)calloc((size_t)n * W, 8);
   uint64_t* next = (uint64_t*)calloc((size_t)n * W, 8);
-  uint64_t* seen = (uint64_t*)calloc((size_t)n * W, 8);
+  /* seen_out, when given, IS the Message-List array (no second n x W copy:
+     32 GiB at 2^26 x 4096) */
+  uint64_t* seen = seen_out;
+  if (seen) memset(seen, 0, (size_t)n * W * 8);
+  else seen = (uint64_t*)calloc((size_t)n * W, 8);
   uint64_t* digest = (uint64_t*)calloc((size_t)n, 8);
   uint8_t* state = (uint8_t*)calloc((size_t)n, 1);
   uint8_t* miss = (uint8_t*)calloc((size_t)n, 1);
@@ -213,6 +218,9 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
   int64_t nrep = 0;
   int32_t r = 0, rounds = 0;
   const uint64_t p_thresh = (p_fail > 0.0 && p_fail < 1.0) ? (uint64_t)ldexp(p_fail, 64) : 0;
+  /* GP_ORACLE_PROGRESS=1: one stderr line per round (long full-size runs) */
+  const char* prog_env = getenv("GP_ORACLE_PROGRESS");
+  const int progress = prog_env && prog_env[0] == '1';
   for (r = 0; r < max_rounds; ++r) {
     or_round_stats st;
     memset(&st, 0, sizeof(st));
@@ -377,9 +385,13 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
     fz = fz_next;
     fz_next = tz;
     rounds = r + 1;
+    if (progress) {
+      fprintf(stderr, "[oracle] round %d: new_bits %lld receivers %lld crashed %lld removals %lld\n", (int)r,
+              (long long)s_new, (long long)s_recv, (long long)st.crashed, (long long)st.removals);
+      fflush(stderr);
+    }
     if (s_new == 0 && r >= last_inject) break;
   }
-  if (seen_out) memcpy(seen_out, seen, (size_t)n * W * 8);
   if (digest_out) memcpy(digest_out, digest, (size_t)n * 8);
   if (coverage_out) {   /* holders of each message: thread-local counts over vertex blocks */
 #pragma omp parallel
@@ -408,7 +420,8 @@ int32_t or_run(int64_t n, const int64_t* row_ptr, const int32_t* col, int32_t di
   if (forwards_out)
     for (int32_t k = 0; k < m; ++k) forwards_out[k] = fwd[k];
   if (n_reports_out) *n_reports_out = nrep;
-  free(front); free(next); free(seen); free(digest); free(state); free(miss);
+  if (seen != seen_out) free(seen);
+  free(front); free(next); free(digest); free(state); free(miss);
   free(deg_live); free(cand); free(fwd); free(fz); free(fz_next); free(acc_t);
   return rounds;
 }

@@ -1,0 +1,155 @@
+"""Child process of tests/test_rccl_standin.py (TEST INFRASTRUCTURE).
+
+Loads the engine built against the in-process RCCL stand-in
+(GOSSIP_HIP_LIB = _build/libgossip_hip_rccl_standin.so, tests/native/
+rccl_standin.cpp) and runs the vertex partition's real RCCL path --
+gp_comm_init, then every round through round_exchange_rccl -> exchange_rccl
+(csrc/partition.hip: the count all-gather, the grouped ncclSend / ncclRecv of
+the boundary entries, the unpack, the counters' all-reduce), and
+gp_finalize_messages' all-reduce -- with P ranks as P threads on one GPU.
+Every output is compared with the oracle's one-context run: per-round
+counters, dead-node reports, first-receipt matrices, digests, Message-Lists,
+coverage and forwards (the reference sends gossip only over real links,
+Peer.py:402-404; liveness Peer.py:298-313, Seed.py:358-406).
+
+Prints "cases ok: N" and exits 0 when every case matches; raises otherwise.
+"""
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import _gossip_pkg  # noqa: E402
+from oracle import lib as oracle  # noqa: E402
+
+STAT_KEYS = ("injected", "lost", "new_bits", "receivers", "sends", "active", "crashed",
+             "reports", "removals", "dup_reports")
+# (push_ratio, unfiltered_pct, flat_max_words): always pull (per-receiver
+# kernel at every width), adaptive direction with unfiltered dense rounds
+MODES = {"pull": (0.0, 0, 0), "adaptive": (10.0, 90, 16)}
+
+
+def run_ranks(pkg, g, origin, inject, P, crashes, cfg):
+    """P threads, rank k driving the context that owns partition k."""
+    uid = pkg.GossipEngine.comm_unique_id()
+    engs = []
+    for k in range(P):
+        e = pkg.GossipEngine(0, **cfg)
+        e.load_graph(g)
+        e.set_partition(k, P)
+        e.set_messages(origin, inject)
+        e.reset()
+        engs.append(e)
+    by_round = {}
+    for v, r in crashes:
+        by_round.setdefault(r, []).append(v)
+    last = int(np.max(inject)) if inject is not None and len(inject) else 0
+    out = [None] * P
+    errs = []
+
+    def rank(k):
+        try:
+            e = engs[k]
+            e.comm_init(uid, P, k)
+            stats, reports = [], []
+            for r in range(254):
+                if r in by_round:
+                    e.crash(by_round[r])   # every rank gets the same global crash list
+                st = e.round()
+                stats.append(st)
+                rep, nrep = e.reports()
+                assert nrep == len(rep)
+                reports.extend(map(tuple, rep.tolist()))
+                if st["new_bits"] == 0 and r >= last:
+                    break
+            e.finalize()   # (an all-reduce of coverage / forwards: every rank at once)
+            out[k] = dict(stats=stats, reports=reports, first=e.first(), digest=e.digest(), seen=e.seen(),
+                          cov=e.coverage(), fwd=e.forwards(), part=e.partition())
+        except BaseException as exc:   # surfaced below, after every thread ended
+            errs.append((k, repr(exc)))
+
+    ts = [threading.Thread(target=rank, args=(k,)) for k in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in engs:
+        e.close()
+    if errs:
+        raise RuntimeError(f"rank failures: {errs}")
+    return out
+
+
+def check(pkg, g, origin, inject, P, crashes, cfg, ref, by_arcs, tag):
+    out = run_ranks(pkg, g, origin, inject, P, crashes, cfg)
+    bounds = pkg.dist.partition_bounds(g.n, P, g.row_ptr if by_arcs else None)
+    assert [o["part"] for o in out] == bounds, (tag, bounds)
+    for o in out:   # counters are all-reduced: every rank holds the global ones
+        assert len(o["stats"]) == ref["rounds"], (tag, len(o["stats"]), ref["rounds"])
+        for a, b in zip(o["stats"], ref["stats"]):
+            for k in STAT_KEYS:
+                assert a[k] == b[k], (tag, k, a["round"], a[k], b[k])
+        assert np.array_equal(o["cov"], ref["coverage"]), tag
+        assert np.array_equal(o["fwd"], ref["forwards"]), tag
+    assert sum(s["xchg_rows"] for s in out[0]["stats"]) > 0, tag
+    reports = sorted(x for o in out for x in o["reports"])
+    assert reports == sorted(map(tuple, ref["reports"].tolist())), tag
+    W = out[0]["seen"].shape[1]
+    assert np.array_equal(np.concatenate([o["first"] for o in out]), ref["first"]), tag
+    assert np.array_equal(np.concatenate([o["digest"] for o in out]), ref["digest"]), tag
+    assert np.array_equal(np.concatenate([o["seen"] for o in out]), ref["seen"][:, :W]), tag
+    return sum(s["xchg_rows"] for s in out[0]["stats"])
+
+
+def main():
+    pkg = _gossip_pkg.load()
+    lib_path = pkg._lib.load()._name
+    assert "rccl_standin" in os.path.basename(lib_path), lib_path
+    print(f"library: {lib_path}", flush=True)
+    cases = 0
+    # small BA overlay: every P, slice rule, churn setting and mode
+    g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
+    origin = pkg.overlay.random_origins(g.n, 200, seed=8)
+    inject = (np.arange(200) % 4).astype(np.int32)
+    for churn in (False, True):
+        kw = dict(churn=True, p_fail=0.02, churn_seed=3) if churn else {}
+        crashes = [(int(origin[5]), 1), (17, 2)] if churn else []
+        ref = oracle.run(g, origin, inject, crashes=crashes, want_first=True, **kw)
+        for mode, (push_ratio, unfiltered_pct, flat_max_words) in MODES.items():
+            for by_arcs in (0, 1):
+                for P in (2, 3, 4):
+                    cfg = dict(track_first=1, track_msg_forwards=int(churn), push_ratio=push_ratio,
+                               unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words,
+                               partition_by_arcs=by_arcs)
+                    if churn:
+                        cfg.update(churn=1, p_fail=0.02, churn_seed=3)
+                    tag = f"ba3001 churn={churn} {mode} by_arcs={by_arcs} P={P}"
+                    t0 = time.time()
+                    rows = check(pkg, g, origin, inject, P, crashes, cfg, ref, by_arcs, tag)
+                    cases += 1
+                    print(f"ok  {tag}: {rows} boundary entries, {time.time() - t0:.2f} s", flush=True)
+    # a Chung-Lu overlay with hubs, W = 64 rows (4096 messages), churn
+    rp, col = oracle.chung_lu(50_000, 10, 2.4, 19)
+    g = pkg.CSR(50_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 4096, seed=19)
+    inject = (np.arange(4096) % 3).astype(np.int32)
+    kw = dict(churn=True, p_fail=0.01, churn_seed=6)
+    ref = oracle.run(g, origin, inject, want_first=True, nthreads=8, **kw)
+    for P, by_arcs in ((2, 1), (4, 0)):
+        cfg = dict(track_first=1, track_msg_forwards=1, churn=1, p_fail=0.01, churn_seed=6, hub_threshold=512,
+                   partition_by_arcs=by_arcs)
+        tag = f"chung-lu 5e4 x 4096 churn P={P} by_arcs={by_arcs}"
+        t0 = time.time()
+        rows = check(pkg, g, origin, inject, P, [], cfg, ref, by_arcs, tag)
+        cases += 1
+        print(f"ok  {tag}: {rows} boundary entries, {time.time() - t0:.2f} s", flush=True)
+    print(f"cases ok: {cases}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

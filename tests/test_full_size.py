@@ -12,10 +12,12 @@ of every vertex, digests, per-message coverage and forwards.  The receive /
 forward logic restated is Peer.py:175-216, 395-408 plus forward-once
 (DESIGN.md §2).
 
-C5: the oracle runs message word 0 -- messages [0, 64) -- and the last word --
-[4032, 4096) -- each as a one-word run, against the engine's one-word runs of
-the same messages (every counter, digests, coverage, forwards and every round's
-dead-node reports).
+C5: the oracle runs ALL 4096 messages with churn, and two engine runs must
+equal it: the run configured exactly as bench.py times it (bench.engine_config:
+no exact frontier rows, so the push gathers whole Message-Lists under
+liveness) -- per-round counters, the Message-List of every vertex, digests,
+coverage and every round's dead-node reports -- and the same run with
+track_msg_forwards = 1, whose per-message forwards are compared too.
 
 Both: the whole 4096-message run is also tied to message shards through the
 composition of DESIGN.md §6: shards [0,64) [64,512) [512,1024) [1024,2048)
@@ -85,38 +87,45 @@ def _run(eng, with_reports=False, report_cap=1 << 24):
     return stats, fps
 
 
-def _check_word(part, ref, w_fps=None):
-    """A one-word engine run (counters, Message-Lists when read, digest,
-    coverage, forwards, per-round report fingerprints) against the oracle's."""
-    assert len(part["stats"]) == ref["rounds"]
-    for a, b in zip(part["stats"], ref["stats"]):
+def _bench_cfg(churn):
+    """The engine configuration bench.py times for this workload (C4 / C5)."""
+    import bench
+    return bench.engine_config(bench.parse(["--workload", "c5" if churn else "c4"]))
+
+
+def _read_run(eng, churn, want_fwd=True):
+    out = dict(dig=eng.digest().copy(), cov=eng.coverage())
+    if want_fwd:
+        out["fwd"] = eng.forwards()
+    return out
+
+
+def _check_counters(stats, ref):
+    assert len(stats) == ref["rounds"]
+    for a, b in zip(stats, ref["stats"]):
         for k in STAT_KEYS:
             assert a[k] == b[k], (k, a["round"], a[k], b[k])
-    if "seen" in part:
-        assert np.array_equal(part["seen"], ref["seen"][:, :1])
-    assert np.array_equal(part["digest"], ref["digest"])
-    assert np.array_equal(part["cov"], ref["coverage"])
-    assert np.array_equal(part["fwd"], ref["forwards"])
-    if part["fps"]:
-        assert ref["n_reports"] <= 1 << 27
-        rep = ref["reports"]
-        for r, fp in enumerate(part["fps"]):
-            assert fp == report_fingerprint(rep[rep[:, 2] == r]), r
-        if w_fps is not None:   # liveness is replicated: the same reports every round
-            k = min(len(part["fps"]), len(w_fps))
-            assert k >= 4 and part["fps"][:k] == w_fps[:k]
+
+
+def _check_seen(seen, ref_seen, n):
+    assert seen.shape == ref_seen.shape
+    for lo in range(0, n, 1 << 20):   # blockwise: no multi-GiB temporaries
+        assert np.array_equal(seen[lo:lo + (1 << 20)], ref_seen[lo:lo + (1 << 20)]), lo
 
 
 def _full_size(pkg, oracle, log2n, seed, churn):
     n, m = 1 << log2n, 4096
-    cfg = dict(track_digest=1)
+    bench_cfg = _bench_cfg(churn)
     okw = {}
     if churn:
-        cfg.update(churn=1, p_fail=0.01, churn_seed=seed, miss_threshold=3, track_msg_forwards=1,
-                   report_capacity=1 << 24)
-        okw = dict(churn=True, p_fail=0.01, churn_seed=seed)
+        bench_cfg["report_capacity"] = 1 << 24   # the reports buffer only: the kernels are unchanged
+        okw = dict(churn=True, p_fail=bench_cfg["p_fail"], churn_seed=bench_cfg["churn_seed"])
+        assert bench_cfg.get("track_msg_forwards", 0) == 0
+    # tracked: the same run with the per-message forwards of every round kept
+    # (exact frontier rows); without churn the bench's run computes them itself
+    trk_cfg = dict(bench_cfg, track_msg_forwards=1) if churn else bench_cfg
     t0 = time.time()
-    whole = pkg.GossipEngine(0, **cfg)
+    whole = pkg.GossipEngine(0, **bench_cfg)
     whole.build_chung_lu(n, 16.0, 2.5, seed)
     _, nnz, _, _ = whole.info()
     chk = whole.check_degree(2.5)
@@ -131,15 +140,29 @@ def _full_size(pkg, oracle, log2n, seed, churn):
     whole.set_messages(origin)
     whole.reset()
     w_stats, w_fps = _run(whole, with_reports=churn)
-    w_dig, w_cov, w_fwd = whole.digest().copy(), whole.coverage(), whole.forwards()
-    w_seen = whole.seen() if not churn else None   # 8 GiB at C4
+    w = _read_run(whole, churn, want_fwd=not churn)
+    w_seen = whole.seen()   # 8 GiB at C4, 32 GiB at C5
     whole.close()
-    _log(f"whole run: {len(w_stats)} rounds in {time.time() - t0:.1f} s")
-    assert sum(s["sends"] for s in w_stats) == int(w_fwd.sum())
-    assert sum(s["injected"] + s["new_bits"] for s in w_stats) == int(w_cov.sum())
+    _log(f"bench-configured run: {len(w_stats)} rounds in {time.time() - t0:.1f} s "
+         f"(scan modes {[s['scan'] for s in w_stats]}, push {[s['mode'] for s in w_stats]})")
+    assert sum(s["injected"] + s["new_bits"] for s in w_stats) == int(w["cov"].sum())
+    if not churn:
+        assert sum(s["sends"] for s in w_stats) == int(w["fwd"].sum())
+
+    t_stats, t_fps, t = w_stats, w_fps, w
+    if churn:   # the same run with exact frontier rows: per-message forwards
+        t0 = time.time()
+        with pkg.GossipEngine(0, **trk_cfg) as trk:
+            trk.load_graph(g)
+            trk.set_messages(origin)
+            trk.reset()
+            t_stats, t_fps = _run(trk, with_reports=True)
+            t = _read_run(trk, churn)
+        _log(f"tracked run: {len(t_stats)} rounds in {time.time() - t0:.1f} s")
+        assert sum(s["sends"] for s in t_stats) == int(t["fwd"].sum())
 
     # message shards on a second context
-    sh = pkg.GossipEngine(0, **cfg)
+    sh = pkg.GossipEngine(0, **trk_cfg)
     sh.load_graph(g)
     parts = []
     for lo, hi in SHARDS:
@@ -155,59 +178,64 @@ def _full_size(pkg, oracle, log2n, seed, churn):
         _log(f"shard [{lo},{hi}) W={sh.words}: {len(stats)} rounds in {time.time() - t0:.1f} s")
     sh.close()
 
-    if not churn:
-        # the whole W = 64 run against the oracle's run of all 4096 messages
-        t0 = time.time()
-        ref = oracle.run(g, origin, nthreads=_threads(), want_first=False)
-        _log(f"oracle, all {m} messages: {ref['rounds']} rounds in {time.time() - t0:.1f} s ({_threads()} threads)")
-        assert len(w_stats) == ref["rounds"]
-        for a, b in zip(w_stats, ref["stats"]):
-            for k in STAT_KEYS:
-                assert a[k] == b[k], (k, a["round"], a[k], b[k])
-        assert w_seen.shape == ref["seen"].shape
-        for lo in range(0, n, 1 << 20):   # blockwise: no 8 GiB temporaries
-            assert np.array_equal(w_seen[lo:lo + (1 << 20)], ref["seen"][lo:lo + (1 << 20)]), lo
-        assert np.array_equal(w_dig, ref["digest"])
-        assert np.array_equal(w_cov, ref["coverage"])
-        assert np.array_equal(w_fwd, ref["forwards"])
-        p0 = parts[0]   # shard [0, 64): its own columns of the oracle's run
-        assert np.array_equal(p0["seen"], ref["seen"][:, :1])
-        assert np.array_equal(p0["cov"], ref["coverage"][:64])
-        assert np.array_equal(p0["fwd"], ref["forwards"][:64])
-        del ref, w_seen
-    else:
-        # one-word runs of the first and the last message word against the oracle
-        ref = oracle.run(g, origin[:64], nthreads=_threads(), want_first=False, report_cap=1 << 27, **okw)
-        _log(f"oracle, word 0: {ref['rounds']} rounds ({_threads()} threads)")
-        _check_word(parts[0], ref, w_fps)
-        del ref
+    # the oracle's run of all 4096 messages (with churn at C5)
+    t0 = time.time()
+    ref = oracle.run(g, origin, nthreads=_threads(), want_first=False, report_cap=1 << 27, **okw)
+    _log(f"oracle, all {m} messages: {ref['rounds']} rounds in {time.time() - t0:.1f} s ({_threads()} threads)")
+    # the bench-configured run, output for output
+    _check_counters(w_stats, ref)
+    _check_seen(w_seen, ref["seen"], n)
+    del w_seen
+    assert np.array_equal(w["dig"], ref["digest"])
+    assert np.array_equal(w["cov"], ref["coverage"])
+    assert np.array_equal(t["fwd"], ref["forwards"])
+    if churn:
+        # every round's dead-node reports (a fingerprinted multiset), both runs
+        assert ref["n_reports"] <= 1 << 27
+        rep = ref["reports"]
+        ref_fps = [report_fingerprint(rep[rep[:, 2] == r]) for r in range(ref["rounds"])]
+        assert w_fps == ref_fps
+        assert t_fps == ref_fps
+        assert sum(s["removals"] for s in w_stats) > 0
+        # the tracked run: counters, digests, coverage
+        _check_counters(t_stats, ref)
+        assert np.array_equal(t["dig"], ref["digest"])
+        assert np.array_equal(t["cov"], ref["coverage"])
+    p0 = parts[0]   # shard [0, 64): its own columns of the oracle's run
+    assert np.array_equal(p0["seen"], ref["seen"][:, :1])
+    assert np.array_equal(p0["cov"], ref["coverage"][:64])
+    assert np.array_equal(p0["fwd"], ref["forwards"][:64])
+    if churn:
+        assert p0["fps"] == ref_fps[:len(p0["fps"])]
+    del ref
 
     # the whole run is the composition of the shards
-    R = len(w_stats)
+    R = len(t_stats)
     assert max(len(p["stats"]) for p in parts) == R
-    for i, s in enumerate(w_stats):
+    for i, s in enumerate(t_stats):
         for k in ("injected", "lost", "new_bits", "sends"):
             assert s[k] == sum(p["stats"][i][k] for p in parts if i < len(p["stats"])), (k, i)
         for k in ("crashed", "reports", "removals", "dup_reports"):
             assert all(p["stats"][i][k] == s[k] for p in parts if i < len(p["stats"])), (k, i)
-    dig = np.zeros_like(w_dig)
+    dig = np.zeros_like(t["dig"])
     for p in parts:
         dig ^= p["digest"]
-    assert np.array_equal(dig, w_dig)
-    assert np.array_equal(np.concatenate([p["cov"] for p in parts]), w_cov)
-    assert np.array_equal(np.concatenate([p["fwd"] for p in parts]), w_fwd)
-    return dict(stats=w_stats, cov=w_cov, fwd=w_fwd, dig=w_dig, g=g, origin=origin, cfg=cfg, fps=w_fps)
+    assert np.array_equal(dig, t["dig"])
+    assert np.array_equal(np.concatenate([p["cov"] for p in parts]), t["cov"])
+    assert np.array_equal(np.concatenate([p["fwd"] for p in parts]), t["fwd"])
+    return dict(stats=w_stats, cov=t["cov"], fwd=t["fwd"], dig=t["dig"], g=g, origin=origin, cfg=bench_cfg,
+                fps=w_fps)
 
 
 @pytest.mark.timeout(900)
 def test_c4_full_size_parity(pkg, oracle):
     """BASELINE config 4 at its own size: 2^24 vertices x 4096 messages, the
-    whole W = 64 run against the oracle's run of all 4096 messages."""
+    bench-configured W = 64 run against the oracle's run of all 4096 messages."""
     out = _full_size(pkg, oracle, 24, 4, churn=False)
     assert out["stats"][-1]["new_bits"] == 0
     # the same run with compact Message-Lists (round 2 through the flat record
     # pull, k_expand_rec): identical to the oracle-checked run
-    with pkg.GossipEngine(0, compact_rows=1, **out["cfg"]) as eng:
+    with pkg.GossipEngine(0, compact_rows=1, **{k: v for k, v in out["cfg"].items() if k != "compact_rows"}) as eng:
         eng.load_graph(out["g"])
         eng.set_messages(out["origin"])
         eng.reset()
@@ -221,24 +249,20 @@ def test_c4_full_size_parity(pkg, oracle):
         assert np.array_equal(eng.digest(), out["dig"])
 
 
-@pytest.mark.timeout(1200)
+@pytest.mark.timeout(1500)
 def test_c5_full_size_parity(pkg, oracle):
     """BASELINE config 5 at its own size: 2^26 vertices x 4096 messages, 1 %/round
-    crashes, 3-miss detection, seed removal."""
+    crashes, 3-miss detection, seed removal (Peer.py:298-313, 395-408,
+    Seed.py:358-406): the bench-configured run and the tracked run against the
+    oracle's run of all 4096 messages."""
     out = _full_size(pkg, oracle, 26, 5, churn=True)
-    assert sum(s["removals"] for s in out["stats"]) > 0
-    # the last message word, [4032, 4096), alone against the oracle and against
-    # the whole run's columns
-    with pkg.GossipEngine(0, **out["cfg"]) as eng:
+    # the last message word, [4032, 4096), as a shard of its own: the whole
+    # run's columns and reports
+    with pkg.GossipEngine(0, **dict(out["cfg"], track_msg_forwards=1)) as eng:
         eng.load_graph(out["g"])
-        eng.configure(msg_word_base=0)   # local word numbers, as the oracle's digest
-        eng.set_messages(out["origin"][4032:])
+        eng.set_message_shard(out["origin"], None, 4032, 4096)
         eng.reset()
         stats, fps = _run(eng, with_reports=True)
-        part = dict(stats=stats, fps=fps, digest=eng.digest().copy(), cov=eng.coverage(), fwd=eng.forwards())
-    ref = oracle.run(out["g"], out["origin"][4032:], nthreads=_threads(), want_first=False, report_cap=1 << 27,
-                     churn=True, p_fail=0.01, churn_seed=5)
-    _log(f"oracle, last word: {ref['rounds']} rounds")
-    _check_word(part, ref, out["fps"])
-    assert np.array_equal(part["cov"], out["cov"][4032:])
-    assert np.array_equal(part["fwd"], out["fwd"][4032:])
+        assert fps == out["fps"][:len(fps)]
+        assert np.array_equal(eng.coverage(), out["cov"][4032:])
+        assert np.array_equal(eng.forwards(), out["fwd"][4032:])

@@ -37,15 +37,24 @@ MODE_IDS = ["pull", "pull-masked", "pull-unfiltered", "push", "adaptive"]
 
 def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096,
              push_ratio=10.0, unfiltered_pct=90, flat_max_words=16, arc_mask_permille=10, prefilter_pct=20,
-             compact_rows=1, summary_min_n=None, **kw):
+             compact_rows=1, summary_min_n=None, track_fwd=None, split_deg=None, **kw):
+    """track_fwd: keep exact frontier rows for per-message forwards (default:
+    with liveness).  track_fwd=0 under churn is bench.py's C5 configuration:
+    no frontier rows, so the push gathers whole Message-Lists under liveness;
+    forwards are then not kept and not compared."""
     churn = kw.get("churn", False)
-    cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(bool(churn or crashes)),
+    live = bool(churn or crashes)
+    if track_fwd is None:
+        track_fwd = int(live)
+    cfg = dict(track_first=int(first), track_digest=1, track_msg_forwards=int(track_fwd),
                churn=int(churn), p_fail=kw.get("p_fail", 0.0), churn_seed=kw.get("churn_seed", 0),
                hub_threshold=hub_threshold, push_ratio=push_ratio,
                unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words,
                arc_mask_permille=arc_mask_permille, prefilter_pct=prefilter_pct, compact_rows=compact_rows)
     if summary_min_n is not None:
         cfg["summary_min_n"] = summary_min_n
+    if split_deg is not None:
+        cfg["split_deg"] = split_deg
     eng = _engine(pkg, g, origin, inject, **cfg)
     by_round = {}
     for v, r in crashes:
@@ -78,7 +87,11 @@ def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_th
         assert np.array_equal(eng.first(), ref["first"])
     assert np.array_equal(eng.digest(), ref["digest"])
     assert np.array_equal(eng.coverage(), ref["coverage"])
-    assert np.array_equal(eng.forwards(), ref["forwards"])
+    if track_fwd or not live:
+        assert np.array_equal(eng.forwards(), ref["forwards"])
+    else:
+        with pytest.raises(pkg.GossipError):   # not kept: refused, never approximated
+            eng.forwards()
     assert sorted(reports) == sorted(map(tuple, ref["reports"].tolist()))
     out = {"stats": stats, "eng": eng, "ref": ref}
     return out
@@ -140,13 +153,36 @@ def test_c1_directed_schedule_and_direct_deliveries(pkg, oracle):
 
 
 @pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
-def test_churn_random(pkg, oracle, mode):
+@pytest.mark.parametrize("track_fwd", [1, 0], ids=["frontier-rows", "bench-c5"])
+def test_churn_random(pkg, oracle, mode, track_fwd):
+    """Random churn, with exact frontier rows (per-message forwards) and
+    without them (bench.py's C5 configuration: the push gathers whole
+    Message-Lists under liveness, the pull keeps no frontier stores)."""
     push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
     g = pkg.overlay.barabasi_albert(5000, 2, seed=5)
     origin = pkg.overlay.random_origins(g.n, 128, seed=5)
     inject = (np.arange(128) % 9).astype(np.int32)
-    r = _compare(pkg, oracle, g, origin, inject, churn=True, p_fail=0.03, churn_seed=77,
+    r = _compare(pkg, oracle, g, origin, inject, churn=True, p_fail=0.03, churn_seed=77, track_fwd=track_fwd,
                  push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask)
+    assert sum(s["removals"] for s in r["stats"]) > 0
+    if push_ratio == 1e-12:
+        assert all(s["mode"] == 1 for s in r["stats"])
+    r["eng"].close()
+
+
+@pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
+@pytest.mark.parametrize("m", [4096, 1000])
+def test_churn_wide_rows_bench_c5(pkg, oracle, mode, m):
+    """bench.py's C5 configuration (no frontier rows) at W = 64 and W = 16 on
+    a Chung-Lu overlay with hubs: pushes of whole Message-Lists under
+    liveness, parked rows, alive sets, sated vertices."""
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
+    rp, col = oracle.chung_lu(60_000, 10, 2.4, 27)
+    g = pkg.CSR(60_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, m, seed=27)
+    r = _compare(pkg, oracle, g, origin, first=False, hub_threshold=512, push_ratio=push_ratio,
+                 unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words, arc_mask_permille=arc_mask,
+                 churn=True, p_fail=0.01, churn_seed=8, track_fwd=0, compact_rows=0)
     assert sum(s["removals"] for s in r["stats"]) > 0
     r["eng"].close()
 
@@ -687,6 +723,58 @@ def test_wide_rows_no_churn(pkg, oracle, mode):
     eng.close()
 
 
+@pytest.mark.parametrize("split_deg", [1, 8, 128, 1 << 20])
+@pytest.mark.parametrize("m,flat_max_words", [(4096, 16), (2048, 16), (512, 0)])
+@pytest.mark.parametrize("churn", [False, True])
+def test_degree_split(pkg, oracle, split_deg, m, flat_max_words, churn):
+    """Degree-split sparse rounds: in a prefiltered pull
+    without early exit, senders of in-degree < split_deg push their rows into
+    the accumulator (k_active_list filter, k_push / k_push_big) and receivers
+    probe only the prefix of their gather-ordered in-list whose senders have
+    in-degree >= split_deg; a touched receiver's accumulator row is one more
+    staged row (hubs: k_hub_final), and k_acc_clear re-zeroes it.  From
+    nothing pushed (1) to everything pushed (2^20), per-receiver kernel at
+    W = 64 / 32 / 8, hubs split over waves, with and without churn: the run
+    equals the oracle's (scan bit 32 marks the split rounds)."""
+    rp, col = oracle.chung_lu(200_000, 10, 2.4, 61)
+    g = pkg.CSR(200_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, m, seed=61)
+    inject = (np.arange(m) % 2).astype(np.int32)
+    kw = dict(churn=True, p_fail=0.01, churn_seed=9) if churn else {}
+    r = _compare(pkg, oracle, g, origin, inject, first=False, hub_threshold=512, push_ratio=1000.0,
+                 unfiltered_pct=90, flat_max_words=flat_max_words, arc_mask_permille=0, prefilter_pct=20,
+                 compact_rows=0, split_deg=split_deg, **kw)
+    scans = [s["scan"] for s in r["stats"]]
+    assert any(x & 32 for x in scans), scans
+    assert all((x & 3) == 3 for x in scans if x & 32), scans
+    r["eng"].close()
+
+
+@pytest.mark.parametrize("push_ratio", [0.0, 100.0], ids=["pull", "adaptive"])
+@pytest.mark.parametrize("schedule", ["round0", "staggered"])
+def test_line_masks(pkg, oracle, push_ratio, schedule):
+    """64-word line masks: filtered pulls without early exit
+    gather only the 128-B lines a sender's nibble names.  The masks come from
+    k_mklm or, in one context without liveness, from the previous round's
+    commits (finish_row / pair_finish ballots, hub receivers OR-ed in after
+    the pull, k_inject's nibbles of the next round's origins): round stats'
+    scan bit 8 = masks read, 16 = masks from the commits.  Both paths must
+    run here, with hubs split over waves and staggered injections, and the
+    run must equal the oracle's."""
+    rp, col = oracle.chung_lu(120_000, 12, 2.4, 52)
+    g = pkg.CSR(120_000, rp, col, False)
+    m = 4096
+    origin = pkg.overlay.random_origins(g.n, m, seed=52)
+    inject = None if schedule == "round0" else (np.arange(m) % 3).astype(np.int32)
+    r = _compare(pkg, oracle, g, origin, inject, first=False, hub_threshold=256, push_ratio=push_ratio,
+                 unfiltered_pct=90, flat_max_words=16, arc_mask_permille=0, prefilter_pct=0, compact_rows=0)
+    scans = [s["scan"] for s in r["stats"]]
+    assert any(x & 8 for x in scans), scans
+    assert any(x & 16 for x in scans), scans
+    assert all(x & 8 for x in scans if x & 16), scans
+    r["eng"].close()
+
+
 @pytest.mark.parametrize("m,flat_max_words", [(4096, 16), (2048, 16), (512, 0), (64, 0)])
 def test_done_in_neighbours(pkg, oracle, m, flat_max_words):
     """Late early-exit rounds without liveness: a receiver whose first in-arcs
@@ -842,16 +930,19 @@ def pkg_oracle_chung_lu(n, dbar, gamma, seed):
 
 
 @pytest.mark.parametrize("prefilter", [0, 20])
-@pytest.mark.parametrize("churn", [False, True])
+@pytest.mark.parametrize("churn", [False, "frontier-rows", "bench-c5"])
 def test_summary_probes(pkg, oracle, prefilter, churn):
     """Summary-level activity probes (one bit per 64 vertices read before the
     bitmap word) forced on at any size: sparse filtered pull rounds, with and
-    without the lane-parallel prefilter, per-receiver kernel, with churn."""
+    without the lane-parallel prefilter, per-receiver kernel, with churn (with
+    and without exact frontier rows: bench.py's C5 runs without)."""
     rp, col = oracle.chung_lu(200_000, 8, 2.5, 21)
     g = pkg.CSR(200_000, rp, col, False)
     origin = pkg.overlay.random_origins(g.n, 256, seed=21)
     inject = (np.arange(256) % 6).astype(np.int32)
     kw = dict(churn=True, p_fail=0.01, churn_seed=5) if churn else {}
+    if churn:
+        kw["track_fwd"] = int(churn == "frontier-rows")
     r = _compare(pkg, oracle, g, origin, inject, push_ratio=0.0, flat_max_words=0, arc_mask_permille=0,
                  prefilter_pct=prefilter, compact_rows=0, summary_min_n=1, **kw)
     # the summary path runs in filtered pull rounds with <= n/256 senders

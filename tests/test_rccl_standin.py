@@ -1,0 +1,60 @@
+"""The vertex partition's RCCL path with P > 1 ranks on one GPU.
+
+RCCL refuses two ranks on one device, so `exchange_rccl` (csrc/partition.hip:
+count all-gather, grouped ncclSend / ncclRecv of the boundary entries, unpack,
+counters' all-reduce) would otherwise first run on an 8-GPU node.  A test
+build of the engine links the in-process stand-in of
+tests/native/rccl_standin.cpp in place of librccl
+(build_lib.build_standin -> _build/libgossip_hip_rccl_standin.so); a child
+process loads it (GOSSIP_HIP_LIB) and drives P = 2, 3, 4 ranks as threads,
+both slice rules, with and without churn, against the oracle
+(tests/rccl_standin_driver.py).  The product library keeps real RCCL.
+Reference: gossip crosses real links only (Peer.py:402-404).
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NCCL_SYMBOLS = ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclGetErrorString", "ncclGroupStart",
+                "ncclGroupEnd", "ncclAllReduce", "ncclAllGather", "ncclSend", "ncclRecv")
+
+
+def _standin_lib(pkg):
+    import importlib
+    sys.path.insert(0, os.path.dirname(pkg._lib.__file__))
+    build_lib = importlib.import_module("build_lib")
+    return build_lib.STANDIN_LIB
+
+
+def test_standin_library_defines_the_rccl_calls(pkg):
+    """CPU: the test build exists, defines every RCCL entry point the engine
+    calls itself and does not pull librccl in; the product library does."""
+    path = _standin_lib(pkg)
+    assert os.path.exists(path), "run __graft_entry__.build()"
+    nm = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    defined = {ln.split()[-1] for ln in nm.splitlines() if ln.strip()}
+    assert set(NCCL_SYMBOLS) <= defined
+    und = subprocess.run(["nm", "-D", "--undefined-only", pkg._lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert set(NCCL_SYMBOLS) <= {ln.split()[-1] for ln in und.splitlines() if ln.strip()}
+    needed = subprocess.run(["readelf", "-d", path], capture_output=True, text=True, check=True).stdout
+    assert "librccl" not in needed
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    assert lib.gp_abi_version() == pkg._lib.ABI_VERSION
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_exchange_rccl_multi_rank(pkg):
+    path = _standin_lib(pkg)
+    assert os.path.exists(path)
+    env = dict(os.environ, GOSSIP_HIP_LIB=path)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "rccl_standin_driver.py")], env=env,
+                       capture_output=True, text=True, timeout=840)
+    print(r.stdout[-6000:])
+    assert r.returncode == 0, r.stderr[-6000:]
+    assert "cases ok: 26" in r.stdout
