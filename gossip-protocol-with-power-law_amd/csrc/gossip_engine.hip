@@ -1043,7 +1043,7 @@ __device__ __forceinline__ bool done_nb(const ExpandArgs& a, int64_t b, int64_t 
 #ifndef GP_DNB_PAIRS
 #define GP_DNB_PAIRS 1
 #endif
-template <int W, class LDS>
+template <int W, bool ALIVE, class LDS>
 __device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
                                           WaveStats& st) {
   static_assert(W == 64, "half-wave rows");
@@ -1065,6 +1065,7 @@ __device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     if (on) {
       if (sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
       cm = load_piece<W>(a.cmask, L.mi[ks], lw);
+      if (ALIVE && a.alive) cm &= load_piece<W>(a.alive, 0, lw);   // liveness: the sated neighbour's alive set
     }
     const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
     const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
@@ -1229,7 +1230,9 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
       if (!need && !hub) a.fpop_next[v] = 0;
       slot_of = a.sp[v];
       if (a.early_exit && need) L.mi[lane] = a.midx[v];
-      if (a.dbits && need) dnb = done_nb(a, b, e);
+      // (with alive sets -- liveness -- only the SCAN_ALIVE variants: the done
+      // target is then cmask & F_r & ~seen, which the others cannot form)
+      if (a.dbits && need && (ALIVE || !a.alive)) dnb = done_nb(a, b, e);
     }
     if constexpr ((MODE & 3) == SCAN_PRE) st.add(S_ARCS, (u64)wave_sum_u32(pre_arcs));
     st.add(S_SENDS, wave_sum_u64(sends));
@@ -1323,14 +1326,17 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
         m &= ~mp;
       }
     }
+    u64 sat = 0;   // receivers of this wave found sated (alive rounds, DESIGN.md §3.4)
     if constexpr (W == 64 && GP_DNB_PAIRS) {
       if (mdn) {   // done in-neighbours: two receivers at a time, the rest below
         const u64 md = m & mdn;
-        dnb_pairs<W>(a, L, md, base, slot_of, st);
+        dnb_pairs<W, ALIVE>(a, L, md, base, slot_of, st);
+        if constexpr (ALIVE) {   // they now hold every alive message of their component: sated too
+          if (a.sate) sat |= md;
+        }
         m &= ~md;
       }
     }
-    u64 sat = 0;   // receivers of this wave found sated (alive rounds, DESIGN.md §3.4)
     while (m) {
       const int k = __ffsll((long long)m) - 1;
       m &= m - 1;
@@ -2404,9 +2410,13 @@ __global__ __launch_bounds__(BLOCK) void k_apply_lanes(ExpandArgs a) {
 // With dbits (single context, early-exit round without liveness) also the done
 // bitmap: bit v = v holds every message of its component (seenpop == done_at,
 // components with messages only), as of the end of the last round.
+// With liveness (sated: the state bytes) the done bitmap is bit v = v is up and
+// sated: it holds every alive message of its component, and
+// the alive sets only shrink once no injection is left.
 __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, u64* __restrict__ abits,
                                                   int64_t n, const uint32_t* __restrict__ seenpop,
-                                                  const uint32_t* __restrict__ done_at, u64* __restrict__ dbits) {
+                                                  const uint32_t* __restrict__ done_at, u64* __restrict__ dbits,
+                                                  const uint8_t* __restrict__ sated) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
   for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
@@ -2416,8 +2426,12 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
     if (dbits) {
       bool d = false;
       if (v < n) {
-        const uint32_t t = done_at[v];
-        d = t != 0u && seenpop[v] == t;
+        if (sated) {
+          d = (sated[v] & (ST_SATED | ST_DOWN)) == ST_SATED;
+        } else {
+          const uint32_t t = done_at[v];
+          d = t != 0u && seenpop[v] == t;
+        }
       }
       const u64 dm = __ballot(d);
       if (lane == 0) dbits[v0 >> 6] = dm;
@@ -2819,6 +2833,9 @@ struct LiveArgs {
   u64* __restrict__ det_base;        // [DET_CAP] first report slot (~0: none)
   u64* __restrict__ partial;
   const int32_t* __restrict__ l2g;   // global id of a local vertex (partitioned; null: identity)
+  uint8_t* __restrict__ lm;          // line masks the last round's commits wrote for this round's
+                                     //   pull (two vertices per byte; null: none): a crash zeroes the
+                                     //   crashed vertex's nibble, as it zeroes its fpop
   int64_t n, vbegin, vend;           // local vertex slots, owned local range
   int64_t report_cap;
   u64 crash_key;
@@ -2861,6 +2878,7 @@ __global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
       }
       uint32_t nsw = sw;
       bool anyc = false;
+      uint32_t crashed_now = 0;   // bit q: vertex v0 + q crashes this round
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int64_t v = v0 + q;
@@ -2873,6 +2891,7 @@ __global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
           if (crash) {
             s = (uint8_t)((s | ST_CRASHED) & ~ST_PENDING);
             a.fpop[v] = 0;   // crash-stop: its frontier is never sent
+            crashed_now |= 1u << q;
             if (v >= a.vbegin && v < a.vend) ncrash += 1;
           }
         }
@@ -2904,6 +2923,19 @@ __global__ __launch_bounds__(BLOCK) void k_churn(LiveArgs a) {
             for (int q = 0; q < 4; ++q)
               if (v0 + q < a.n) a.miss[v0 + q] = (uint8_t)(nmw >> (8 * q));
           }
+        }
+      }
+      if (crashed_now && a.lm) {   // this lane's 4 vertices are the 2 bytes at v0 / 2 (v0 % 4 == 0)
+        uint32_t keep = 0xFFFFu;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if ((crashed_now >> q) & 1u) keep &= ~(0xFu << (4 * q));
+        if (full) {
+          uint16_t* p = reinterpret_cast<uint16_t*>(a.lm) + (v0 >> 2);
+          *p = (uint16_t)(*p & keep);
+        } else {
+          for (int q = 0; q < 4; ++q)
+            if (v0 + q < a.n && ((crashed_now >> q) & 1u)) a.lm[(v0 + q) >> 1] &= (uint8_t)((q & 1) ? 0x0Fu : 0xF0u);
         }
       }
       if (nsw != sw) {
@@ -3412,7 +3444,7 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.prehi = c->split_now ? c->d_prehi : nullptr;
   a.split_push = 0;
   a.acc_row = c->split_now ? c->acc_row : 0;
-  a.lm = c->lines_now ? (c->lm_written_prev && !alive_on(c) ? c->d_lmw[c->cur] : c->d_lm) : nullptr;
+  a.lm = c->lines_now ? (c->lm_written_prev ? c->d_lmw[c->cur] : c->d_lm) : nullptr;
   a.lm_next = c->lm_write_now ? c->d_lmw[c->cur ^ 1] : nullptr;
   a.cmk = c->cml_read_now ? c->d_cmk[c->cur] : nullptr;
   a.cml = c->cml_read_now ? c->d_cml[c->cur] : nullptr;
@@ -3712,9 +3744,22 @@ static int launch_expand(Ctx* c) {
   c->dnb_now = GP_DONE_NB && c->early_exit_now && !c->mode_push && !c->liveness_active && !c->local &&
                c->nloc() == c->n_alloc && c->words > c->cfg.flat_max_words &&
                (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m;
+  // With liveness the done bitmap is the sated marks (up and sated: holds every
+  // alive message of its component; k_mkbits): a receiver with such an
+  // in-neighbour receives exactly cmask & F_r & ~seen, since every bit of it
+  // lies in that neighbour's frontier (it sent everything older while both were
+  // up, and crashes are final).  From the round after the first marking round.
+#ifndef GP_DONE_NB_LIVE
+#define GP_DONE_NB_LIVE 0
+#endif
+  if (GP_DONE_NB_LIVE && !c->dnb_now && c->liveness_active && alive_on(c) && c->early_exit_now && !c->mode_push &&
+      !c->local && c->nloc() == c->n_alloc && c->words > c->cfg.flat_max_words && c->sate_since >= 0 &&
+      c->round > c->sate_since)
+    c->dnb_now = true;
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
                      dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc,
-                     c->d_seenpop, c->d_done_at, c->dnb_now ? c->d_dbits : nullptr);
+                     c->d_seenpop, c->d_done_at, c->dnb_now ? c->d_dbits : nullptr,
+                     c->dnb_now && c->liveness_active ? (const uint8_t*)c->d_state : nullptr);
   // filtered pull: probe every arc inside the scan, or build the per-arc mask
   // first (pays once the probes are many: senders >= arc_mask_permille of n)
   c->arc_mask_now = !c->mode_push && !c->unfiltered_now && c->cfg.arc_mask_permille > 0 &&
@@ -3755,16 +3800,20 @@ static int launch_expand(Ctx* c) {
   c->lines_now = GP_LINE_MASKS && c->words == 64 && c->d_lm != nullptr && !c->mode_push && !c->unfiltered_now &&
                  !c->arc_mask_now && !c->early_exit_now && c->n_alloc <= (int64_t(1) << 27);   // (u << 4) | lines
   // this round's 64-word pull commits write the next round's masks: one
-  // context without liveness (a crash zeroes a sender's fpop, not its mask;
-  // ghosts' rows come from the exchange), per-receiver kernel, no records
+  // context (ghosts' rows come from the exchange), per-receiver kernel, no
+  // records; under liveness k_churn zeroes a crashing sender's nibble with
+  // its fpop (round 4 of the build; k_mklm ran there until then)
 #ifndef GP_LM_WRITE
 #define GP_LM_WRITE 1
 #endif
   // (only sparse rounds: a line-mask round follows a round with few new bits,
   // and early-exit rounds would pay the commits' extra stores for nothing --
   // C4 rounds 3-4 +0.3 ms when every pull wrote them)
+#ifndef GP_LM_WRITE_LIVE
+#define GP_LM_WRITE_LIVE 0
+#endif
   c->lm_write_now = GP_LM_WRITE && c->words == 64 && c->d_lmw[0] != nullptr && !c->mode_push &&
-                    !c->early_exit_now && !c->liveness_active && !c->local && !c->cml_read_now &&
+                    !c->early_exit_now && !c->local && !c->cml_read_now && (GP_LM_WRITE_LIVE || !c->liveness_active) &&
                     !c->cml_write_now;
   // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
   c->prefilter_now = !c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.prefilter_pct > 0 &&
@@ -3799,6 +3848,7 @@ static int launch_expand(Ctx* c) {
 #define GP_SATE 1
 #endif
   a.sate = GP_SATE && alive_on(c) && c->early_exit_now && c->round >= c->last_inject_round ? 1 : 0;
+  if (a.sate && c->sate_since < 0) c->sate_since = c->round;
   c->lines_ran = c->lines_from_commits = false;
   switch (c->words) {
     case 1: launch_expand_w<1>(c, a); break;
@@ -4177,7 +4227,10 @@ void gp_default_config(gp_config* cfg) {
   cfg->flat_max_words = 16;
   cfg->summary_min_n = 1ll << 25;   // activity bitmap > 4 MB: outgrows an XCD's L2
   cfg->partition_by_arcs = 0;       // vertex partitions: equal vertex counts (1: equal arc counts)
-  cfg->split_deg = 128;             // degree-split sparse rounds
+#ifndef GP_SPLIT_DEG_DEFAULT
+#define GP_SPLIT_DEG_DEFAULT 128
+#endif
+  cfg->split_deg = GP_SPLIT_DEG_DEFAULT;   // degree-split sparse rounds
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -4506,6 +4559,7 @@ int gp_reset(gp_ctx* c) {
   c->cml_written_prev = false;
   c->cml_read_now = c->cml_write_now = false;
   c->lm_written_prev = c->lm_write_now = false;
+  c->sate_since = -1;
   GP_HIP(hipMemsetAsync(c->d_miss, 0, na, s));
   GP_HIP(hipMemsetAsync(c->d_deg_live, 0, na * 4, s));
   GP_HIP(hipMemcpyAsync(c->d_deg_live, c->d_deg_out, (size_t)c->n_alloc * 4, hipMemcpyDeviceToDevice, s));
@@ -4576,6 +4630,7 @@ static int round_launch(Ctx* c) {
     la.stats = stats;
     la.partial = partial;
     la.l2g = c->local ? c->d_l2g : nullptr;
+    la.lm = c->lm_written_prev ? c->d_lmw[c->cur] : nullptr;
     la.n = c->n_alloc;
     la.vbegin = 0;
     la.vend = c->nloc();

@@ -149,6 +149,7 @@ struct Ctx {
   // last round (done in-neighbours)
   u64* d_dbits = nullptr;
   bool dnb_now = false;             // this round's pull reads d_dbits
+  int32_t sate_since = -1;          // first round that marked sated vertices (-1: none yet this run)
   // [n_alloc] line masks (W = 64): bit l = 128-B line l of v's
   // row in this round's slot holds a nonzero word; 0 = not a sender.  Built by
   // k_mklm from the very rows the round's filtered pull reads (SCAN_LINES)
