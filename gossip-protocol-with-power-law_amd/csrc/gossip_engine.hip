@@ -955,9 +955,7 @@ __device__ __forceinline__ u64x2 pair_seen(const ExpandArgs& a, int h, int lw, b
 
 // SCAN_PRE rounds without early exit (round 1 of a C4 run: 7.9 M receivers,
 // about 2 active in-neighbours each, already found by the lane phase)
-// (LINES: line-mask rounds -- the staged entries are (u << 4) | lines and a
-// lane loads its 16-B piece only when its 128-B line is named)
-template <int W, bool LINES, class LDS>
+template <int W, class LDS>
 __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
                                           WaveStats& st) {
   static_assert(W == 64, "half-wave rows");
@@ -979,33 +977,18 @@ __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
     u64x2 acc = {0, 0};
     const uint32_t nmax = max(npA, npB);
-    uint32_t lines = 0;   // LINES: 128-B lines this half loaded (lane lw == 0 of each half counts)
     for (uint32_t q0 = 0; q0 < nmax; q0 += GP_PAIR_RIF) {
       u64x2 r[GP_PAIR_RIF];
 #pragma unroll
       for (int q = 0; q < GP_PAIR_RIF; ++q) {
         r[q] = u64x2{0, 0};
-        if (q0 + q < np) {
-          const int32_t e = L.pre[ks][q0 + q];
-          if constexpr (LINES) {
-            if ((e >> (lw >> 3)) & 1) r[q] = load_piece<W>(a.rows, e >> 4, lw);
-            lines += (uint32_t)__popc((uint32_t)e & 15u);
-          } else {
-            r[q] = load_piece<W>(a.rows, e, lw);
-          }
-        }
+        if (q0 + q < np) r[q] = load_piece<W>(a.rows, L.pre[ks][q0 + q], lw);
       }
 #pragma unroll
       for (int q = 0; q < GP_PAIR_RIF; ++q) acc |= r[q];
     }
     st.add(S_GATHERED, (u64)(npA + npB));
-    if constexpr (LINES) {
-      const uint32_t lA = (uint32_t)__builtin_amdgcn_readlane((int)lines, 0);
-      const uint32_t lB = kB >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)lines, 32) : 0u;
-      st.add(S_ROW_BYTES, (u64)(lA + lB) * 128ull);
-    } else {
-      st.add(S_ROW_BYTES, (u64)(npA + npB) * (u64)(8 * W));
-    }
+    st.add(S_ROW_BYTES, (u64)(npA + npB) * (u64)(8 * W));
     const u64x2 sv = pair_seen<W>(a, h, lw, on, kB, v, sv_slot, acc, st);
     pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, acc, sv, st);
   }
@@ -1182,21 +1165,6 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
               u64 w[PRE_IDS];
 #pragma unroll
               for (int q = 0; q < PRE_IDS; ++q) c[q] = h * PRE_IDS + q < deg ? a.gcol[b + h * PRE_IDS + q] : -1;
-              if constexpr ((MODE & SCAN_LINES) != 0) {
-                // line-mask rounds: the probe reads the sender's nibble (0: not a
-                // sender) and the staged entry carries it, (u << 4) | lines
-                uint32_t lv[PRE_IDS];
-#pragma unroll
-                for (int q = 0; q < PRE_IDS; ++q) lv[q] = c[q] >= 0 ? (uint32_t)lm_of(a.lm, c[q]) : 0u;
-#pragma unroll
-                for (int q = 0; q < PRE_IDS; ++q) {
-                  if (lv[q]) {
-                    if (cnt < (uint32_t)PRE_IDS) L.pre[lane][cnt] = (c[q] << 4) | (int32_t)lv[q];
-                    ++cnt;
-                  }
-                }
-                continue;
-              }
 #if GP_SUMMARY_PROBE
               if (a.sbits) {   // summary level first: L2-resident, most probes end there
                 u64 sw[PRE_IDS];
@@ -1272,11 +1240,6 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
           }
         }
         u64 w[GP_WAVE_PRE_N];
-        uint32_t lq[GP_WAVE_PRE_N];   // line-mask rounds: the senders' nibbles
-        if constexpr ((MODE & SCAN_LINES) != 0) {
-#pragma unroll
-          for (int q = 0; q < GP_WAVE_PRE_N; ++q) lq[q] = c[q] >= 0 ? (uint32_t)lm_of(a.lm, c[q]) : 0u;
-        } else
 #if GP_SUMMARY_PROBE
         if (a.sbits) {
           u64 sw[GP_WAVE_PRE_N];
@@ -1292,19 +1255,12 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
 #pragma unroll
         for (int q = 0; q < GP_WAVE_PRE_N; ++q) {
           if (kq[q] < 0) continue;
-          bool act;
-          int32_t ent = c[q];
-          if constexpr ((MODE & SCAN_LINES) != 0) {
-            act = lq[q] != 0u;
-            ent = (c[q] << 4) | (int32_t)lq[q];
-          } else {
-            act = c[q] >= 0 && ((w[q] >> (c[q] & 63)) & 1ull);
-          }
+          const bool act = c[q] >= 0 && ((w[q] >> (c[q] & 63)) & 1ull);
           const u64 am = __ballot(act);
           const int tq = (int)((tw >> kq[q]) & 1ull);   // degree-split: + the accumulator row
           const int cnt = __popcll(am) + tq;
           if (cnt <= PRE_IDS) {   // (more: the serial loop scans it, and counts its arcs)
-            if (act) L.pre[kq[q]][lane_rank(am)] = ent;
+            if (act) L.pre[kq[q]][lane_rank(am)] = c[q];
             if (lane == 0) {
               if (tq) L.pre[kq[q]][cnt - 1] = a.acc_row + (int32_t)(base + kq[q]);
               L.np[kq[q]] = (uint8_t)cnt;
@@ -1322,7 +1278,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
     if constexpr (GP_PRE_PAIRS && W == 64 && (MODE & 3) == SCAN_PRE) {
       if (!ee) {   // prefiltered receivers two at a time, the rest below
         const u64 mp = m & __ballot(need && L.np[lane] != 0xFFu);
-        pre_pairs<W, (MODE & SCAN_LINES) != 0>(a, L, mp, base, slot_of, st);
+        pre_pairs<W>(a, L, mp, base, slot_of, st);
         m &= ~mp;
       }
     }
@@ -1382,10 +1338,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::v
       } else if constexpr ((MODE & 3) == SCAN_PRE) {
         const uint32_t np = L.np[k];
         if (np != 0xFFu) {
-          if constexpr (W == 64 && (MODE & SCAN_LINES) != 0)
-            gather_lines<GP_LINES_RIF>(a, L.pre[k], (int)np, g, lw, acc, st);   // (u << 4) | lines entries
-          else
-            gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
+          gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
         } else {
           gather_scan<W, SCAN>(a, vb, vb + L.len[k], L, lane, g, lw, acc, st, ee, want, col0);
           if ((tw >> k) & 1ull) {   // degree-split: the accumulator row (not staged: a scanned receiver)
@@ -1644,6 +1597,13 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       st.add(S_VISITED, (u64)__popcll(needm));
     }
     const bool need = (needm >> lane) & 1ull;
+    // degree-split rounds: the receivers the push half touched (bit r =
+    // receiver base + r; NR = 32 waves take their half of the 64-vertex word)
+    u64 tw = 0;
+    if (a.prehi) {
+      tw = a.tbits[base >> 6] >> (base & 63);
+      if constexpr (NR < 64) tw &= (1ull << NR) - 1ull;
+    }
     // (a wave with no receiver to scan is done: late rounds leave most waves
     // with none, and the passes and the receiver side cost latency even empty)
     if (needm != 0ull) {
@@ -1667,7 +1627,8 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       int64_t start = 0;
       if ((todo >> lane) & 1ull) {
         const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
-        const uint32_t deg = (uint32_t)(e - b);
+        // (degree-split rounds, no early exit: the prefix of bigger senders)
+        const uint32_t deg = a.prehi ? (uint32_t)a.prehi[v] : (uint32_t)(e - b);
         sdeg = deg > lo ? min(deg, hi) - lo : 0u;
         start = b + lo;
       }
@@ -1710,8 +1671,9 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       wave_sync_lds();
       todo = __ballot(((longm >> lane) & 1ull) && F.rd[lane]);
     }
-    st.add(S_GATHERED, gathered);
-    st.add(S_ROW_BYTES, gathered * (u64)(8 * W));
+    const u64 tn = (u64)__popcll(tw & needm);   // accumulator rows read by the receiver side
+    st.add(S_GATHERED, gathered + tn);
+    st.add(S_ROW_BYTES, (gathered + tn) * (u64)(8 * W));
     // receiver side: RPI receivers per wave-instruction, LPR lanes x 16 B per
     // row (coalesced, like the gather); a receiver with nothing new reads and
     // writes nothing.  Per-receiver words go to F.tot / F.dig, then one
@@ -1727,6 +1689,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
       if (rn) {
         accp.x = F.acc[r][lw * WPL];
         if constexpr (WPL == 2) accp.y = F.acc[r][lw * WPL + 1];
+        if ((tw >> r) & 1ull) accp |= load_piece<W>(a.acc, rv, lw);   // degree-split: the pushed rows
       }
       const bool any = group_or<LPR>((accp.x | accp.y) != 0ull);
       u64x2 sv = {0, 0};
@@ -3576,13 +3539,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   // line masks of the senders' rows (SCAN_LINES; inside the pull's events and bytes)
   const bool lines = W == 64 && a.lm != nullptr && !flat && !masked && mode == SCAN_FILTERED && !a.cmk &&
                      !a.cmk_next && !c->prefilter_now && !(a.alive && a.early_exit);
-  // line-mask rounds probe the in-lists of low-degree receivers in the lane
-  // phase (the prefilter's machinery, all probes of the wave in flight at once)
-  // and gather them two receivers at a time: the per-receiver chain of column
-  // ids -> probes -> rows is the bound of these rounds
-#ifndef GP_LINES_PRE
-#define GP_LINES_PRE 0
-#endif
+
   if (lines && a.lm == c->d_lm)   // (the last round's commits did not write them)
     hipLaunchKernelGGL(k_mklm, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
                        dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], a.rows, c->n_alloc, c->d_lm, a.partial);
@@ -3635,12 +3592,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
         }
       }
       if constexpr (W == 64) {
-        if (!done && lines && GP_LINES_PRE) {   // low-degree receivers probed lane-parallel
-          hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_LINES>), grid, dim3(BLOCK), 0, c->stream, a);
-          c->lines_ran = true;
-          c->lines_from_commits = a.lm != c->d_lm;
-          done = true;
-        } else if (!done && lines) {
+        if (!done && lines) {
           hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_LINES>), grid, dim3(BLOCK), 0, c->stream, a);
           c->lines_ran = true;
           c->lines_from_commits = a.lm != c->d_lm;
@@ -3710,6 +3662,15 @@ static int launch_expand(Ctx* c) {
 #endif
   const double ratio = c->cfg.push_ratio * (c->words <= GP_NARROW_PUSH_MAXW && early ? GP_NARROW_PUSH_SCALE : 1.0);
   c->mode_push = c->cfg.push_ratio > 0.0 && est * ratio <= (double)c->nnz;
+  // narrow rows: a round that pushes only because of the narrow scale pulls
+  // as a degree-split round instead when that is on (its prefix probes are a
+  // fraction of the arcs, its push half only the low-degree senders' arcs)
+#ifndef GP_SPLIT_NARROW
+#define GP_SPLIT_NARROW 1
+#endif
+  if (GP_SPLIT_NARROW && c->mode_push && c->cfg.split_deg > 0 && !c->local && c->nloc() == c->n_alloc &&
+      est * c->cfg.push_ratio > (double)c->nnz)
+    c->mode_push = false;
   c->push_est = est;
   if (c->mode_push && c->nloc() > 0)
     GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1], 0, (size_t)c->nloc() * 4, c->stream));
@@ -3750,7 +3711,7 @@ static int launch_expand(Ctx* c) {
   // lies in that neighbour's frontier (it sent everything older while both were
   // up, and crashes are final).  From the round after the first marking round.
 #ifndef GP_DONE_NB_LIVE
-#define GP_DONE_NB_LIVE 0
+#define GP_DONE_NB_LIVE 1
 #endif
   if (GP_DONE_NB_LIVE && !c->dnb_now && c->liveness_active && alive_on(c) && c->early_exit_now && !c->mode_push &&
       !c->local && c->nloc() == c->n_alloc && c->words > c->cfg.flat_max_words && c->sate_since >= 0 &&
@@ -3810,7 +3771,7 @@ static int launch_expand(Ctx* c) {
   // and early-exit rounds would pay the commits' extra stores for nothing --
   // C4 rounds 3-4 +0.3 ms when every pull wrote them)
 #ifndef GP_LM_WRITE_LIVE
-#define GP_LM_WRITE_LIVE 0
+#define GP_LM_WRITE_LIVE 1
 #endif
   c->lm_write_now = GP_LM_WRITE && c->words == 64 && c->d_lmw[0] != nullptr && !c->mode_push &&
                     !c->early_exit_now && !c->local && !c->cml_read_now && (GP_LM_WRITE_LIVE || !c->liveness_active) &&
@@ -3824,8 +3785,7 @@ static int launch_expand(Ctx* c) {
   // low-degree minority of a degree-biased sender set), receivers probe only
   // the gather-order prefix of bigger senders
   c->split_now = c->cfg.split_deg > 0 && c->prefilter_now && !c->early_exit_now && !c->local &&
-                 c->nloc() == c->n_alloc && !c->cml_read_now && !c->cml_write_now &&
-                 !(c->words <= 32 && c->words <= c->cfg.flat_max_words);
+                 c->nloc() == c->n_alloc && !c->cml_read_now && !c->cml_write_now;
   if (c->split_now) {   // accumulator rows as rows of this round's slot buffer (same stride)
     const ptrdiff_t d = reinterpret_cast<const char*>(c->d_acc) - reinterpret_cast<const char*>(c->d_slot[c->cur]);
     const ptrdiff_t rb = (ptrdiff_t)c->words * 8;

@@ -724,7 +724,7 @@ def test_wide_rows_no_churn(pkg, oracle, mode):
 
 
 @pytest.mark.parametrize("split_deg", [1, 8, 128, 1 << 20])
-@pytest.mark.parametrize("m,flat_max_words", [(4096, 16), (2048, 16), (512, 0)])
+@pytest.mark.parametrize("m,flat_max_words", [(4096, 16), (2048, 16), (512, 0), (512, 16), (64, 16)])
 @pytest.mark.parametrize("churn", [False, True])
 def test_degree_split(pkg, oracle, split_deg, m, flat_max_words, churn):
     """Degree-split sparse rounds: in a prefiltered pull
@@ -734,8 +734,9 @@ def test_degree_split(pkg, oracle, split_deg, m, flat_max_words, churn):
     in-degree >= split_deg; a touched receiver's accumulator row is one more
     staged row (hubs: k_hub_final), and k_acc_clear re-zeroes it.  From
     nothing pushed (1) to everything pushed (2^20), per-receiver kernel at
-    W = 64 / 32 / 8, hubs split over waves, with and without churn: the run
-    equals the oracle's (scan bit 32 marks the split rounds)."""
+    W = 64 / 32 / 8 and the edge-parallel kernel at W = 8 / 1 (whose receiver
+    side ORs the accumulator rows), hubs split over waves, with and without
+    churn: the run equals the oracle's (scan bit 32 marks the split rounds)."""
     rp, col = oracle.chung_lu(200_000, 10, 2.4, 61)
     g = pkg.CSR(200_000, rp, col, False)
     origin = pkg.overlay.random_origins(g.n, m, seed=61)
@@ -865,8 +866,10 @@ def test_compact_message_lists(pkg, oracle, prefilter, churn):
     r["eng"].close()
     if churn:
         return
+    # (the same work without records: degree-split rounds off, as record rounds never split)
     with pkg.GossipEngine(0, track_digest=1, push_ratio=0.0, prefilter_pct=prefilter, compact_rows=0,
-                          arc_mask_permille=0, unfiltered_pct=90, flat_max_words=16, hub_threshold=4096) as eng:
+                          arc_mask_permille=0, unfiltered_pct=90, flat_max_words=16, hub_threshold=4096,
+                          split_deg=0) as eng:
         eng.load_graph(g)
         eng.set_messages(origin)
         eng.reset()
