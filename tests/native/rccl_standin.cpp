@@ -117,6 +117,15 @@ size_t esize_of(ncclDataType_t t) {
   }
 }
 
+// every copy runs on the calling rank's own stream and is waited for: a plain
+// hipMemcpy does not order against the engine's non-blocking streams (device-to-
+// device and pageable host-to-device copies may return before the data lands),
+// so its next kernel could read a receive buffer the copy has not filled yet
+bool copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return true;
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s) == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+}
+
 bool sync_streams(const std::vector<Op>& ops) {
   for (const Op& o : ops)
     if (hipStreamSynchronize(o.stream) != hipSuccess) return false;
@@ -160,15 +169,14 @@ ncclResult_t run_collectives(ncclComm* comm, std::vector<Op>& coll) {
       for (int r = 0; r < w->n; ++r) {
         const Op& x = (*w->posted[(size_t)r])[ci];
         in[(size_t)r].resize(x.count * x.esize);
-        if (x.count && hipMemcpy(in[(size_t)r].data(), x.src, x.count * x.esize, hipMemcpyDefault) != hipSuccess)
-          rc = ncclSystemError;
+        if (!copy(in[(size_t)r].data(), x.src, x.count * x.esize, o.stream)) rc = ncclSystemError;
       }
     if (!barrier(w)) return ncclSystemError;
     if (rc == ncclSuccess && o.count) {
       if (o.kind == OP_ALLGATHER) {
         for (int r = 0; r < w->n; ++r)
-          if (hipMemcpy(static_cast<uint8_t*>(o.dst) + (size_t)r * o.count * o.esize, in[(size_t)r].data(),
-                        o.count * o.esize, hipMemcpyDefault) != hipSuccess)
+          if (!copy(static_cast<uint8_t*>(o.dst) + (size_t)r * o.count * o.esize, in[(size_t)r].data(),
+                    o.count * o.esize, o.stream))
             rc = ncclSystemError;
       } else {   // all-reduce: sum of u64 (the only reduction the engine asks for)
         std::vector<uint64_t> acc(o.count, 0);
@@ -176,7 +184,7 @@ ncclResult_t run_collectives(ncclComm* comm, std::vector<Op>& coll) {
           const uint64_t* x = reinterpret_cast<const uint64_t*>(in[(size_t)r].data());
           for (size_t i = 0; i < o.count; ++i) acc[i] += x[i];
         }
-        if (hipMemcpy(o.dst, acc.data(), o.count * 8, hipMemcpyDefault) != hipSuccess) rc = ncclSystemError;
+        if (!copy(o.dst, acc.data(), o.count * 8, o.stream)) rc = ncclSystemError;
       }
     }
     if (!barrier(w)) return ncclSystemError;
@@ -219,7 +227,7 @@ ncclResult_t run_p2p(ncclComm* comm, const std::vector<Op>& p2p) {
       q.pop_front();
     }
     bool ok = m.bytes == o.count * o.esize;
-    if (ok && m.bytes) ok = hipMemcpy(o.dst, m.src, m.bytes, hipMemcpyDefault) == hipSuccess;
+    if (ok && m.bytes) ok = copy(o.dst, m.src, m.bytes, o.stream);
     if (!ok) rc = m.bytes == o.count * o.esize ? ncclSystemError : ncclInvalidUsage;
     {
       std::lock_guard<std::mutex> lk(w->mu);
