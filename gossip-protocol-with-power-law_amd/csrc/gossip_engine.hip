@@ -446,29 +446,6 @@ __device__ __forceinline__ uint8_t lm_of(const uint8_t* __restrict__ lm, int32_t
   if constexpr (GP_LM_NIBBLE) return (uint8_t)((lm[u >> 1] >> ((u & 1) * 4)) & 0xF);
   else return lm[u];
 }
-// GP_LM2 (experiment): the line-mask round probes a 2-bit code per vertex
-// (4 MB at 2^24 instead of 8: 0 = not a sender, 1 = line 0, 2 = lines 0-1,
-// 3 = all four), a superset of the nibble's lines built from it per round
-#ifndef GP_LM2
-#define GP_LM2 0
-#endif
-__device__ __forceinline__ uint8_t lm2_of(const uint8_t* __restrict__ lm2, int32_t u) {
-  const uint32_t c = (lm2[u >> 2] >> ((u & 3) * 2)) & 3u;
-  return (uint8_t)((c == 3u) ? 15u : (c == 2u ? 3u : c));
-}
-__global__ __launch_bounds__(256) void k_lm2(const uint8_t* __restrict__ nib, int64_t nbytes4, uint8_t* __restrict__ lm2) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // lm2 byte i: vertices 4i .. 4i + 3
-  if (i >= nbytes4) return;
-  const uint32_t b = (uint32_t)nib[2 * i] | ((uint32_t)nib[2 * i + 1] << 8);
-  uint32_t out = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t x = (b >> (4 * q)) & 15u;
-    const uint32_t c = x == 0u ? 0u : (x == 1u ? 1u : ((x & 12u) == 0u ? 2u : 3u));
-    out |= c << (2 * q);
-  }
-  lm2[i] = (uint8_t)out;
-}
 // 4-bit line mask from a ballot over 32 lanes of 16 B (8 lanes per 128-B line)
 __device__ __forceinline__ uint32_t lines_of(uint32_t b) {
   uint32_t l = 0;
@@ -714,7 +691,7 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
       int32_t u = -1;
       if (lane < n) {
         u = (col0 != INT32_MIN && j0 == b) ? col0 : a.gcol[j0 + lane];
-        lv = GP_LM2 ? lm2_of(a.lm, u) : lm_of(a.lm, u);
+        lv = lm_of(a.lm, u);
       }
       const u64 ml = __ballot(lv != 0);
       if (lv) L.idx[lane_rank(ml)] = (u << 4) | (int32_t)lv;
@@ -832,12 +809,13 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   if constexpr (W == 64 && CMLW) {
     if (a.cml_next) dense = write_rec(a.cml_next, v, g, lw, sv | nw);
   }
-  uint32_t lmn = 0;   // W = 64: the lines of the new row holding a nonzero word (lm_next)
+  // W = 64: the lines of the new bits -- the frontier the next round sends --
+  // holding a nonzero word (lm_next).  Gathering only those lines of a
+  // sender's Message-List is exact: the rest of the row was sent before (a
+  // superset such as k_mklm's whole-row lines is exact too)
+  uint32_t lmn = 0;
   if constexpr (W == 64) {
-    if (a.lm_next) {
-      const u64x2 row = sv | nw;
-      lmn = lines_of((uint32_t)__ballot(g == 0 && (row.x | row.y) != 0ull));
-    }
+    if (a.lm_next) lmn = lines_of((uint32_t)__ballot(g == 0 && (nw.x | nw.y) != 0ull));
   }
   if (g == 0) {
     alive_add<W>(a, L, lw, nw);
@@ -942,11 +920,8 @@ __device__ __forceinline__ void pair_finish(const ExpandArgs& a, LDS& L, int h, 
   }
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) t ^= __shfl_xor(t, o);
-  uint32_t lmn = 0;   // lines of the new row holding a nonzero word (lm_next)
-  if (a.lm_next) {
-    const u64x2 row = sv | nw;
-    lmn = lines_of((uint32_t)(__ballot(on && (row.x | row.y) != 0ull) >> (32 * h)));
-  }
+  uint32_t lmn = 0;   // lines of the new bits holding a nonzero word (lm_next; finish_row)
+  if (a.lm_next) lmn = lines_of((uint32_t)(__ballot(on && (nw.x | nw.y) != 0ull) >> (32 * h)));
   if (lw == 0 && on && tot) {
     L.tot[ks] = tot;
     L.lmn[ks] = (uint8_t)lmn;
@@ -3567,11 +3542,6 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   if (lines && a.lm == c->d_lm)   // (the last round's commits did not write them)
     hipLaunchKernelGGL(k_mklm, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
                        dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], a.rows, c->n_alloc, c->d_lm, a.partial);
-  if (GP_LM2 && lines && c->d_lm2) {   // (experiment) the 2-bit codes of this round's masks
-    const int64_t nb4 = (c->n_alloc + 3) / 4;
-    hipLaunchKernelGGL(k_lm2, dim3((unsigned)((nb4 + 255) / 256)), dim3(256), 0, c->stream, a.lm, nb4, c->d_lm2);
-    a.lm = c->d_lm2;
-  }
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
     const dim3 grid(grid_for(a.nloc, (int64_t)WAVES * FlatNR<W>::value));
     if constexpr (W <= 32) {
@@ -3803,7 +3773,8 @@ static int launch_expand(Ctx* c) {
 #define GP_LM_WRITE_LIVE 1
 #endif
   c->lm_write_now = GP_LM_WRITE && c->words == 64 && c->d_lmw[0] != nullptr && !c->mode_push &&
-                    !c->early_exit_now && !c->local && !c->cml_read_now && (GP_LM_WRITE_LIVE || !c->liveness_active) &&
+                    !c->early_exit_now && !c->local && !c->cml_read_now &&
+                    (GP_LM_WRITE_LIVE || !c->liveness_active) &&
                     !c->cml_write_now;
   // sparse filtered pull: the lane phase probes the in-lists of low-degree receivers
   c->prefilter_now = !c->mode_push && !c->unfiltered_now && !c->arc_mask_now && c->cfg.prefilter_pct > 0 &&
@@ -3950,7 +3921,7 @@ static void free_state(Ctx* c) {
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_det_big); dfree(&c->d_det_pre); dfree(&c->d_det_live); dfree(&c->d_det_cur); dfree(&c->d_det_base);
-  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_lm2); dfree(&c->d_lmw[0]); dfree(&c->d_lmw[1]); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_lmw[0]); dfree(&c->d_lmw[1]); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);
   dfree(&c->d_midx); dfree(&c->d_cmask);
@@ -4064,8 +4035,6 @@ static int alloc_state(Ctx* c) {
   GP_TRY(dalloc(&c->d_dbits, (na + 63) / 64));
   dfree(&c->d_lm);
   if (c->words == 64) GP_TRY(dalloc(&c->d_lm, GP_LM_NIBBLE ? (na + 1) / 2 + 32 : na));
-  dfree(&c->d_lm2);
-  if (GP_LM2 && c->words == 64) GP_TRY(dalloc(&c->d_lm2, (na + 3) / 4 + 64));
   for (int k = 0; k < 2; ++k) {
     dfree(&c->d_lmw[k]);
     if (c->words == 64 && GP_LM_NIBBLE) GP_TRY(dalloc(&c->d_lmw[k], (na + 1) / 2 + 64));
@@ -4258,7 +4227,7 @@ void gp_destroy(gp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
-  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_lm2); dfree(&c->d_lmw[0]); dfree(&c->d_lmw[1]); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
+  dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_lmw[0]); dfree(&c->d_lmw[1]); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
   dfree(&c->d_gcol); dfree(&c->d_prehi); dfree(&c->d_midx); dfree(&c->d_cmask);
   dfree(&c->d_acc); dfree(&c->d_tbits); dfree(&c->d_nbits); dfree(&c->d_touched); dfree(&c->d_active); dfree(&c->d_big);

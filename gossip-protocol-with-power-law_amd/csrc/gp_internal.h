@@ -154,7 +154,6 @@ struct Ctx {
   // row in this round's slot holds a nonzero word; 0 = not a sender.  Built by
   // k_mklm from the very rows the round's filtered pull reads (SCAN_LINES)
   uint8_t* d_lm = nullptr;
-  uint8_t* d_lm2 = nullptr;         // GP_LM2 experiment: 2-bit line codes, n_alloc / 4 bytes
   bool lines_now = false;
   // [2][n_alloc / 2] the same masks written by the commits of a 64-word pull
   // for the next round's senders (nibbles, by round parity like d_fpop): a
