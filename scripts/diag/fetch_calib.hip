@@ -65,6 +65,27 @@ __global__ void k_rand_rows(const uint8_t* __restrict__ p, int64_t nitems_buf, i
   if ((acc.x | acc.y) == 0x123456789ull) sink[0] = acc.x;
 }
 
+// the line-mask round's pattern: GROUP lanes read a random 128-B line of the
+// big buffer (a row piece) and lane 0 of the group probes one random byte of a
+// small table (the nibble array, 8 MiB at C4: past one XCD's L2, inside the
+// Infinity Cache).  FETCH_SIZE minus k_rand_rows<8>'s for the same count is
+// what the probes cost at the memory-side counters.
+__global__ void k_rows_probe(const uint8_t* __restrict__ p, int64_t nitems_buf, const uint8_t* __restrict__ tab,
+                             int64_t tab_lines, int64_t n, u64 seed, u64* __restrict__ sink) {
+  const int lane = threadIdx.x & 63;
+  const int g = lane / 8, lw = lane % 8;
+  u64x2 acc = {0, 0};
+  u64 t = 0;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = wave * 8 + g; i < n; i += nwaves * 8) {
+    const u64 h = mix(seed + (u64)i);
+    acc |= *reinterpret_cast<const u64x2*>(p + (int64_t)(h % (u64)nitems_buf) * 128 + lw * 16);
+    if (lw == 0) t += tab[(int64_t)((h >> 32) % (u64)tab_lines) * 128 + (h & 127)];
+  }
+  if ((acc.x | acc.y | t) == 0x123456789ull) sink[0] = acc.x;
+}
+
 int main() {
   const size_t bytes = size_t(4) << 30;
   uint8_t* buf = nullptr;
@@ -85,13 +106,26 @@ int main() {
   hipLaunchKernelGGL(k_rand_rows<8>, dim3(grid), dim3(block), 0, 0, buf, lines, int64_t(1) << 24, 33ull, sink);
   hipLaunchKernelGGL(k_rand_rows<32>, dim3(grid), dim3(block), 0, 0, buf, (int64_t)(bytes / 512), int64_t(1) << 22,
                      44ull, sink);
+  // an 8 MiB table (65536 lines) at the end of the buffer, probed 2^24 times
+  // with 1-byte loads, twice (the second pass finds it warm in the Infinity
+  // Cache): counted per probe if the memory-side counters see L3 hits
+  const int64_t tab_lines = 65536;
+  const uint8_t* tab = buf + bytes - tab_lines * 128;
+  hipLaunchKernelGGL(k_rand<1>, dim3(grid), dim3(block), 0, 0, tab, tab_lines, int64_t(1) << 24, 66ull, sink);
+  hipLaunchKernelGGL(k_rand<1>, dim3(grid), dim3(block), 0, 0, tab, tab_lines, int64_t(1) << 24, 77ull, sink);
+  // rows alone, then rows with a probe of the table each (the line-mask round)
+  hipLaunchKernelGGL(k_rand_rows<8>, dim3(grid), dim3(block), 0, 0, buf, lines - tab_lines, int64_t(1) << 24, 88ull,
+                     sink);
+  hipLaunchKernelGGL(k_rows_probe, dim3(grid), dim3(block), 0, 0, buf, lines - tab_lines, tab, tab_lines,
+                     int64_t(1) << 24, 99ull, sink);
   if (hipDeviceSynchronize() != hipSuccess) {
     fprintf(stderr, "kernel failed\n");
     return 1;
   }
   printf("expected bytes touched: stream16 %zu, rand1 %lld lines, rand8 %lld lines, row64 (first half of) %lld lines, line128 %lld lines, "
-         "row512 %lld rows (x4 lines)\n",
-         size_t(1) << 30, 1ll << 24, 1ll << 24, 1ll << 24, 1ll << 24, 1ll << 22);
+         "row512 %lld rows (x4 lines); then rand1 on an 8 MiB table x2, line128 alone and with a table probe each, "
+         "%lld each\n",
+         size_t(1) << 30, 1ll << 24, 1ll << 24, 1ll << 24, 1ll << 24, 1ll << 22, 1ll << 24);
   hipFree(buf);
   hipFree(sink);
   return 0;
