@@ -263,11 +263,7 @@ constexpr int CML_MAXW = CML_WORDS - 1;   // nonzero words a record holds
 #ifndef GP_EXPAND_WAVES
 #define GP_EXPAND_WAVES 0
 #endif
-#if GP_EXPAND_WAVES > 0
-#define EXPAND_BOUNDS __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GP_EXPAND_WAVES)))
-#else
 #define EXPAND_BOUNDS __launch_bounds__(BLOCK)
-#endif
 // rows each lane keeps in flight per gather step (MLP vs VGPRs)
 #ifndef GP_ROWS_IN_FLIGHT
 #define GP_ROWS_IN_FLIGHT 4
@@ -1099,12 +1095,20 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, LDS& L, int
 #ifndef GP_ALIVE_WAVES
 #define GP_ALIVE_WAVES 0
 #endif
-template <int MODE>
+// the same for W < 64 (message shards, C3 widths; 0: the compiler's choice):
+// 8 on the 2048-message shard (W = 32) 37.6 -> 41.1 ms (r04_ab_waves.txt)
+#ifndef GP_NARROW_WAVES
+#define GP_NARROW_WAVES 0
+#endif
+template <int W, int MODE>
 struct ExpandWaves {
-  static constexpr int value = (MODE & SCAN_ALIVE) != 0 && GP_ALIVE_WAVES > 0 ? GP_ALIVE_WAVES : 1;
+  static constexpr int value = (MODE & SCAN_ALIVE) != 0 && GP_ALIVE_WAVES > 0 ? GP_ALIVE_WAVES
+                               : W < 64 && GP_NARROW_WAVES > 0                ? GP_NARROW_WAVES
+                               : GP_EXPAND_WAVES > 0                          ? GP_EXPAND_WAVES
+                                                                              : 1;
 };
 template <int W, int MODE>
-__global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<MODE>::value))) void k_expand(ExpandArgs a) {
+__global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<W, MODE>::value))) void k_expand(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
   __shared__ LDS_OF(MODE) s_w[WAVES];
   const int lane = threadIdx.x & 63;
