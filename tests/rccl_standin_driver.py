@@ -140,7 +140,7 @@ def main():
     inject = (np.arange(4096) % 3).astype(np.int32)
     kw = dict(churn=True, p_fail=0.01, churn_seed=6)
     ref = oracle.run(g, origin, inject, want_first=True, nthreads=8, **kw)
-    for P, by_arcs in ((2, 1), (4, 0)):
+    for P, by_arcs in ((2, 1), (4, 0), (8, 1)):   # P = 8: the node's rank count
         cfg = dict(track_first=1, track_msg_forwards=1, churn=1, p_fail=0.01, churn_seed=6, hub_threshold=512,
                    partition_by_arcs=by_arcs)
         tag = f"chung-lu 5e4 x 4096 churn P={P} by_arcs={by_arcs}"

@@ -1,7 +1,7 @@
 """The multi-process launch of bench.py on the GPU box: real engine processes
 (one context each, both on cuda:0 of the one-GPU box) over dist.py's TCP
-control plane, message shards.  The 2-rank whole-job
-edge-deliveries must equal the 1-rank run's, and neither process may load
+control plane, message shards.  The 2-, 4- and 8-rank
+whole-job edge-deliveries must equal the 1-rank run's, and neither process may load
 PyTorch."""
 import json
 import os
@@ -44,13 +44,16 @@ def _launch(world, extra=()):
     return lines[0]
 
 
-def test_two_process_message_shards():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_multi_process_message_shards(world):
+    """world ranks as the driver launches them at N = world (here all on the
+    box's one GPU): the whole-job counters equal the one-process run's."""
     one = _launch(1)
-    two = _launch(2)
-    assert two["n_gpus"] == 2 and "message-shard x2" in two["config"]["parallelism"]
+    many = _launch(world)
+    assert many["n_gpus"] == world and f"message-shard x{world}" in many["config"]["parallelism"]
     for k in ("n", "arcs", "messages", "edge_deliveries_per_step", "rounds_per_step"):
-        assert two["config"][k] == one["config"][k], k
-    assert two["config"]["words_per_row"] == 32 and one["config"]["words_per_row"] == 64
+        assert many["config"][k] == one["config"][k], k
+    assert many["config"]["words_per_row"] == 64 // world and one["config"]["words_per_row"] == 64
 
 
 def test_bench_process_loads_no_torch():

@@ -6,7 +6,7 @@ counters' all-reduce) would otherwise first run on an 8-GPU node.  A test
 build of the engine links the in-process stand-in of
 tests/native/rccl_standin.cpp in place of librccl
 (build_lib.build_standin -> _build/libgossip_hip_rccl_standin.so); a child
-process loads it (GOSSIP_HIP_LIB) and drives P = 2, 3, 4 ranks as threads,
+process loads it (GOSSIP_HIP_LIB) and drives P = 2, 3, 4 (and 8 on the hub overlay) ranks as threads,
 both slice rules, with and without churn, against the oracle
 (tests/rccl_standin_driver.py).  The product library keeps real RCCL.
 Reference: gossip crosses real links only (Peer.py:402-404).
@@ -57,4 +57,4 @@ def test_exchange_rccl_multi_rank(pkg):
                        capture_output=True, text=True, timeout=840)
     print(r.stdout[-6000:])
     assert r.returncode == 0, r.stderr[-6000:]
-    assert "cases ok: 26" in r.stdout
+    assert "cases ok: 27" in r.stdout
