@@ -538,6 +538,53 @@ def test_edge_cases(pkg, oracle, mode):
     _compare(pkg, oracle, star, np.full(100, 5, np.int32), hub_threshold=64, **kw)["eng"].close()
 
 
+@pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
+def test_raw_csr_self_loops_and_repeated_arcs(pkg, oracle, mode):
+    """An in-CSR loaded as given (gp_load_graph): self-loops and repeated arcs
+    count as links in the sends (deg) but can never bring a vertex anything
+    it does not hold; unsorted in-lists; W = 2 rows, hubs split at 64."""
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
+    g0 = pkg.overlay.barabasi_albert(3000, 3, seed=41)
+    rng = np.random.default_rng(41)
+    src, dst = g0.arcs()
+    loops = rng.choice(g0.n, 300, replace=False)
+    again = rng.choice(src.size, 2000, replace=False)   # repeated arcs, both directions
+    s = np.concatenate([src, loops, src[again], dst[again]])
+    d = np.concatenate([dst, loops, dst[again], src[again]])
+    order = rng.permutation(s.size)   # in-lists in no particular order
+    s, d = s[order], d[order]
+    rp = np.zeros(g0.n + 1, np.int64)
+    np.add.at(rp, d + 1, 1)
+    rp = np.cumsum(rp)
+    col = np.empty(s.size, np.int32)
+    cur = rp[:-1].copy()
+    for u, v in zip(s.tolist(), d.tolist()):
+        col[cur[v]] = u
+        cur[v] += 1
+    g = pkg.CSR(g0.n, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 100, seed=41)
+    inject = (np.arange(100) % 3).astype(np.int32)
+    kw = dict(push_ratio=push_ratio, unfiltered_pct=unfiltered_pct, flat_max_words=flat_max_words,
+              arc_mask_permille=arc_mask, hub_threshold=64)
+    _compare(pkg, oracle, g, origin, inject, **kw)["eng"].close()
+    _compare(pkg, oracle, g, origin, inject, churn=True, p_fail=0.05, churn_seed=41, **kw)["eng"].close()
+
+
+@pytest.mark.parametrize("p_fail", [0.3, 1.0])
+@pytest.mark.parametrize("mode", MODES, ids=MODE_IDS)
+def test_extreme_churn(pkg, oracle, mode, p_fail):
+    """A third of the live vertices crash every round, or all of them at once:
+    detection, removals and lost messages at their limits, W = 64 rows."""
+    push_ratio, unfiltered_pct, flat_max_words, arc_mask = mode
+    g = pkg.overlay.barabasi_albert(4000, 3, seed=43)
+    origin = pkg.overlay.random_origins(g.n, 4096, seed=43)
+    inject = (np.arange(4096) % 4).astype(np.int32)
+    for track_fwd in (1, 0):
+        _compare(pkg, oracle, g, origin, inject, first=False, track_fwd=track_fwd, churn=True, p_fail=p_fail,
+                 churn_seed=43, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct,
+                 flat_max_words=flat_max_words, arc_mask_permille=arc_mask, hub_threshold=256)["eng"].close()
+
+
 def test_full_size_invariants_c3(pkg):
     """Size-independent properties at a large size: conservation of sends and
     receipts, idempotence of a repeated run."""
