@@ -73,6 +73,15 @@ def parse(argv=None):
                     help="N > 1: message shards (no data-path collective, default) or the vertex "
                          "partition with a sparse boundary exchange every round (ncclSend/Recv of "
                          "the boundary vertices' new words)")
+    ap.add_argument("--shard-assign", choices=("interleaved", "blocked", "wordsnake"), default="blocked",
+                    help="message shards: blocks of the table ordered by spread speed as a whole (blocked, "
+                         "default: rank 0 the fastest; a rank's receivers complete together), every rank a "
+                         "contiguous block of the drawn table ordered inside it (interleaved: every rank gets "
+                         "messages of every speed), or the ordered table's 64-message words dealt in snake "
+                         "order (wordsnake); DESIGN.md §6, profiles/r04_shard_emulation.txt")
+    ap.add_argument("--emulate-shard", default=None, metavar="R/N",
+                    help="one process runs rank R's message shard of an N-rank job alone (the per-GPU work "
+                         "of the N-GPU run, for projections on a one-GPU box; not a multi-GPU number)")
     ap.add_argument("--profile-steps", action="store_true",
                     help="print per-round stats of the last step to stderr")
     a = ap.parse_args(argv)
@@ -233,6 +242,14 @@ def main():
     dist = pkg.dist
     world, rank, local = dist.env()
     pg = dist.init()
+    emu = None
+    if args.emulate_shard:   # rank R of an N-rank message-shard job, alone in this process
+        if world > 1:
+            raise SystemExit("--emulate-shard runs one process")
+        er, en = (int(x) for x in args.emulate_shard.split("/"))
+        if not (en >= 1 and 0 <= er < en):
+            raise SystemExit("--emulate-shard R/N needs 0 <= R < N")
+        emu = (er, en)
     n = 1 << args.log2n
     # one GPU per rank; on a smaller box (rehearsal) ranks share devices round-robin
     device = local % max(pkg._lib.device_count(), 1)
@@ -245,19 +262,30 @@ def main():
     # SURVEY.md §8a A9 on the overlay just built (outside the timed region)
     deg = eng.check_degree(args.gamma)
     t0 = time.perf_counter()
-    shards = world > 1 and args.parallel == "messages"
+    s_world, s_rank = (emu[1], emu[0]) if emu else (world, rank)   # the message-shard job's ranks
+    shards = s_world > 1 and (emu is not None or args.parallel == "messages")
     origin = pkg.overlay.random_origins(n, args.messages, seed=args.seed)
     if args.message_order == "spread":   # bit order by spread speed; setup, untimed
-        # within each rank's shard, so that every rank gets messages of every speed
-        blocks = ([dist.message_shard(args.messages, world, p) for p in range(world)] if shards
-                  else [(0, args.messages)])
+        # blocked (default): the whole table, then cut, so that each rank's
+        # messages spread at one speed and its receivers complete together (the
+        # N = 8 job's slowest rank 22.3 -> 13.4 ms against interleaved: within
+        # each rank's block of the drawn table); DESIGN.md §6
+        blocks = ([dist.message_shard(args.messages, s_world, p) for p in range(s_world)]
+                  if shards and args.shard_assign == "interleaved" else [(0, args.messages)])
         origin = np.concatenate([origin[lo:hi][eng.spread_order(origin[lo:hi], hops=args.spread_hops)]
                                  for lo, hi in blocks])
+        if shards and args.shard_assign == "wordsnake":   # word k of the ordered table to rank snake(k)
+            words = [origin[64 * k:64 * (k + 1)] for k in range((args.messages + 63) // 64)]
+            per = [[] for _ in range(s_world)]
+            for k, w in enumerate(words):
+                r, lap = k % s_world, k // s_world
+                per[r if lap % 2 == 0 else s_world - 1 - r].append(w)
+            origin = np.concatenate([np.concatenate(x) for x in per if x])
     if world > 1 and not shards:
         eng.set_partition(rank, world)
         eng.comm_init(dist.share_comm_id(pg, pkg.GossipEngine.comm_unique_id), world, rank)
     if shards:   # this rank's word-aligned block of the 4096 messages
-        lo, hi = dist.message_shard(args.messages, world, rank)
+        lo, hi = dist.message_shard(args.messages, s_world, s_rank)
         eng.set_message_shard(origin, None, lo, hi)
     else:
         eng.set_messages(origin)
@@ -308,7 +336,7 @@ def main():
                                                 "crashed", "reports", "removals", "scan", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not emu and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, eng, origin, pkg)
     if rank == 0:
         out = {
@@ -332,7 +360,10 @@ def main():
                        "message_order": (f"spread ({args.spread_hops}-hop key)" if args.message_order == "spread"
                                          else "given"),
                        "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,
-                       "parallelism": (f"message-shard x{world} (no data-path collective)" if shards else
+                       "parallelism": (f"message-shard {emu[0]} of {emu[1]} alone (the per-GPU work of the "
+                                       f"{emu[1]}-GPU run, {args.shard_assign})" if emu else
+                                       f"message-shard x{world} (no data-path collective, {args.shard_assign})"
+                                       if shards else
                                        f"vertex-partition x{world}" + (" (sparse boundary exchange, ncclSend/Recv)"
                                                                       if world > 1 else "")),
                        "setup_s": round(setup_s, 2), "build_s": round(build_s, 2),
