@@ -58,6 +58,8 @@ def parse(argv=None):
     ap.add_argument("--split-deg", type=int, default=128,
                     help="degree-split sparse rounds: senders of in-degree < this push, receivers probe the "
                          "gather-order prefix of the others (0 = off; DESIGN.md §3.2)")
+    ap.add_argument("--split-max-permille", type=int, default=10,
+                    help="degree-split rounds only while fewer than this many vertices per 1000 send")
     ap.add_argument("--flat-max-words", type=int, default=16,
                     help="rows of at most this many words take the edge-parallel pull (<= 32, 0 = never)")
     ap.add_argument("--message-order", choices=("given", "spread"), default="spread",
@@ -126,7 +128,8 @@ def engine_config(args):
     cfg = dict(track_digest=1, track_first=0, hub_threshold=args.hub_threshold, push_ratio=args.push_ratio,
                early_exit=args.early_exit, unfiltered_pct=args.unfiltered_pct, flat_max_words=args.flat_max_words,
                arc_mask_permille=args.arc_mask_permille, compact_rows=args.compact_rows,
-               prefilter_pct=args.prefilter_pct, summary_min_n=args.summary_min_n, split_deg=args.split_deg)
+               prefilter_pct=args.prefilter_pct, summary_min_n=args.summary_min_n, split_deg=args.split_deg,
+               split_max_permille=args.split_max_permille)
     if args.workload == "c5":   # Bernoulli crashes of live vertices, stream seeded by the run seed
         cfg.update(churn=1, p_fail=args.p_fail, churn_seed=args.seed, miss_threshold=3)
     return cfg

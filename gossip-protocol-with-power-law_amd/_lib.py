@@ -90,6 +90,7 @@ class Config(ctypes.Structure):
         ("summary_min_n", ctypes.c_int64),
         ("partition_by_arcs", ctypes.c_int32),
         ("split_deg", ctypes.c_int32),
+        ("split_max_permille", ctypes.c_int32),
     ]
 
 
@@ -129,7 +130,7 @@ SIGNATURES = {
     "gp_checkpoint_load": (ctypes.c_int, [_P, _P, _I64]),
 }
 
-ABI_VERSION = 16   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 17   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

@@ -3788,8 +3788,13 @@ static int launch_expand(Ctx* c) {
   // senders of in-degree < split_deg push (few arcs: they are the
   // low-degree minority of a degree-biased sender set), receivers probe only
   // the gather-order prefix of bigger senders
+  // Only while the senders are a sliver of the vertices (C4 / C5 round 1:
+  // 0.1-0.4 %): the 512-message shards' round 2, prefiltered with 7-13 % of
+  // the vertices sending, pushed 30-67 M low-degree arcs in 3.3-5.9 ms
+  // against a 1.8-1.9 ms pull half (profiles/r04_split_cap.txt)
   c->split_now = c->cfg.split_deg > 0 && c->prefilter_now && !c->early_exit_now && !c->local &&
-                 c->nloc() == c->n_alloc && !c->cml_read_now && !c->cml_write_now;
+                 c->nloc() == c->n_alloc && !c->cml_read_now && !c->cml_write_now &&
+                 senders * 1000.0 < (double)c->cfg.split_max_permille * (double)c->n;
   if (c->split_now) {   // accumulator rows as rows of this round's slot buffer (same stride)
     const ptrdiff_t d = reinterpret_cast<const char*>(c->d_acc) - reinterpret_cast<const char*>(c->d_slot[c->cur]);
     const ptrdiff_t rb = (ptrdiff_t)c->words * 8;
@@ -4194,7 +4199,11 @@ void gp_default_config(gp_config* cfg) {
 #ifndef GP_SPLIT_DEG_DEFAULT
 #define GP_SPLIT_DEG_DEFAULT 128
 #endif
+#ifndef GP_SPLIT_MAX_PERMILLE
+#define GP_SPLIT_MAX_PERMILLE 10
+#endif
   cfg->split_deg = GP_SPLIT_DEG_DEFAULT;   // degree-split sparse rounds
+  cfg->split_max_permille = GP_SPLIT_MAX_PERMILLE;   // ... while senders are a sliver
 }
 
 int gp_create(int device, gp_ctx** out) {
@@ -4266,6 +4275,7 @@ int gp_configure(gp_ctx* c, const gp_config* cfg) {
   if (cfg->partition_by_arcs != 0 && cfg->partition_by_arcs != 1)
     return set_error(GP_EINVAL, "partition_by_arcs must be 0 or 1");
   if (cfg->split_deg < 0) return set_error(GP_EINVAL, "split_deg must be >= 0");
+  if (cfg->split_max_permille < 0) return set_error(GP_EINVAL, "split_max_permille must be >= 0");
   if (c->local && cfg->partition_by_arcs != c->cfg.partition_by_arcs)
     return set_error(GP_ESTATE, "a partitioned context keeps its partition: reload the overlay to change it");
   GP_HIP(hipSetDevice(c->device));

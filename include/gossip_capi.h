@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 16
+#define GP_ABI_VERSION 17
 
 typedef struct gp_ctx gp_ctx;
 
@@ -150,6 +150,9 @@ typedef struct gp_config {
                                   the accumulator) and receivers probe only the prefix of
                                   their gather-ordered in-list whose senders have
                                   in-degree >= split_deg (0 = off; single-rank contexts) */
+  int32_t split_max_permille;  /* ... only while fewer than this many vertices per 1000
+                                  send (default 10: the push half grows with the low-
+                                  degree senders; 1000 = whenever prefiltered; ABI 17)   */
 } gp_config;
 
 /* what for gp_read */

@@ -37,7 +37,7 @@ MODE_IDS = ["pull", "pull-masked", "pull-unfiltered", "push", "adaptive"]
 
 def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_threshold=4096,
              push_ratio=10.0, unfiltered_pct=90, flat_max_words=16, arc_mask_permille=10, prefilter_pct=20,
-             compact_rows=1, summary_min_n=None, track_fwd=None, split_deg=None, **kw):
+             compact_rows=1, summary_min_n=None, track_fwd=None, split_deg=None, split_max_permille=None, **kw):
     """track_fwd: keep exact frontier rows for per-message forwards (default:
     with liveness).  track_fwd=0 under churn is bench.py's C5 configuration:
     no frontier rows, so the push gathers whole Message-Lists under liveness;
@@ -55,6 +55,8 @@ def _compare(pkg, oracle, g, origin, inject=None, crashes=(), first=True, hub_th
         cfg["summary_min_n"] = summary_min_n
     if split_deg is not None:
         cfg["split_deg"] = split_deg
+    if split_max_permille is not None:
+        cfg["split_max_permille"] = split_max_permille
     eng = _engine(pkg, g, origin, inject, **cfg)
     by_round = {}
     for v, r in crashes:
@@ -791,7 +793,7 @@ def test_degree_split(pkg, oracle, split_deg, m, flat_max_words, churn):
     kw = dict(churn=True, p_fail=0.01, churn_seed=9) if churn else {}
     r = _compare(pkg, oracle, g, origin, inject, first=False, hub_threshold=512, push_ratio=1000.0,
                  unfiltered_pct=90, flat_max_words=flat_max_words, arc_mask_permille=0, prefilter_pct=20,
-                 compact_rows=0, split_deg=split_deg, **kw)
+                 compact_rows=0, split_deg=split_deg, split_max_permille=1000, **kw)
     scans = [s["scan"] for s in r["stats"]]
     assert any(x & 32 for x in scans), scans
     assert all((x & 3) == 3 for x in scans if x & 32), scans
