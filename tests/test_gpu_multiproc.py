@@ -1,6 +1,6 @@
 """The multi-process launch of bench.py on the GPU box: real engine processes
 (one context each, both on cuda:0 of the one-GPU box) over dist.py's TCP
-control plane, message shards.  The 2-, 4- and 8-rank
+control plane, message shards.  The 2- and 4-rank
 whole-job edge-deliveries must equal the 1-rank run's, and neither process may load
 PyTorch."""
 import json
@@ -44,7 +44,7 @@ def _launch(world, extra=()):
     return lines[0]
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 4])   # (the N = 8 launch is the driver's alone)
 def test_multi_process_message_shards(world):
     """world ranks as the driver launches them at N = world (here all on the
     box's one GPU): the whole-job counters equal the one-process run's."""
