@@ -47,8 +47,21 @@ int copy_sync(Ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind ki
 typedef unsigned long long u64;
 typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 
-constexpr int BLOCK = 256;         // 4 waves
+#ifndef GP_BLOCK
+#define GP_BLOCK 256
+#endif
+constexpr int BLOCK = GP_BLOCK;    // 4 waves (GP_BLOCK: experiment builds)
 constexpr int WAVES = BLOCK / 64;
+constexpr int GS = 256 / BLOCK;     // grid-stride kernels' blocks per CU scale: same threads per CU at every BLOCK
+// the per-receiver and edge-parallel pull kernels run in blocks of their own
+// size: one wave per block, so that a CU slot frees as soon as its wave ends
+// instead of waiting for the block's slowest wave (C4 47.4-47.6 -> 44.5-45.4
+// ms, C5 222-225 -> 210-216 ms; profiles/r04_ab_block.txt)
+#ifndef GP_EXPAND_BLOCK
+#define GP_EXPAND_BLOCK 64
+#endif
+constexpr int EBLOCK = GP_EXPAND_BLOCK;
+constexpr int EWAVES = EBLOCK / 64;
 constexpr int NPART = 2048;        // partial stat slots (spread the atomics)
 
 // ---------------------------------------------------------------------------
@@ -129,7 +142,8 @@ __device__ void flush_stats(const WaveStats& s, u64* __restrict__ partial) {
   if (threadIdx.x < NST) {
     u64 t = 0;
 #pragma unroll
-    for (int w = 0; w < WAVES; ++w) t += red[w * NST + threadIdx.x];
+    for (int w = 0; w < WAVES; ++w)
+      if (w < (int)(blockDim.x >> 6)) t += red[w * NST + threadIdx.x];   // (pull kernels: EWAVES)
     if (t) atomicAdd(&partial[(size_t)threadIdx.x * NPART + (blockIdx.x % NPART)], t);
   }
 }
@@ -263,7 +277,7 @@ constexpr int CML_MAXW = CML_WORDS - 1;   // nonzero words a record holds
 #ifndef GP_EXPAND_WAVES
 #define GP_EXPAND_WAVES 0
 #endif
-#define EXPAND_BOUNDS __launch_bounds__(BLOCK)
+#define EXPAND_BOUNDS __launch_bounds__(EBLOCK)
 // rows each lane keeps in flight per gather step (MLP vs VGPRs)
 #ifndef GP_ROWS_IN_FLIGHT
 #define GP_ROWS_IN_FLIGHT 4
@@ -1110,7 +1124,7 @@ struct ExpandWaves {
 template <int W, int MODE>
 __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<W, MODE>::value))) void k_expand(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
-  __shared__ LDS_OF(MODE) s_w[WAVES];
+  __shared__ LDS_OF(MODE) s_w[EWAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
@@ -1119,7 +1133,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(ExpandWaves<W, MODE>
   constexpr int SCAN = MODE & ~SCAN_ALIVE;
   WaveStats st;
   ws_zero(st);
-  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * 64;
+  const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * 64;
   if (base < a.nloc) {
     const int64_t li = base + lane;
     bool need = false, act = false, dnb = false;
@@ -1560,11 +1574,11 @@ __device__ __forceinline__ u64 flat_pass(const ExpandArgs& a, FlatLds<W>& F, int
 #endif
 
 template <int W, int MODE, bool EE>
-__global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
+__global__ __launch_bounds__(EBLOCK) void k_expand_flat(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
   constexpr int RPI = Geo<W>::RPI;
   constexpr int WPL = Geo<W>::WPL;
-  __shared__ FlatLds<W> s_f[WAVES];
+  __shared__ FlatLds<W> s_f[EWAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
@@ -1572,7 +1586,7 @@ __global__ __launch_bounds__(BLOCK) void k_expand_flat(ExpandArgs a) {
   constexpr int NR = FlatNR<W>::value;
   WaveStats st;
   ws_zero(st);
-  const int64_t base = ((int64_t)blockIdx.x * WAVES + wib) * NR;
+  const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * NR;
   if (base < a.nloc) {
     alive_zero<W>(a, F.alive, lane);
     // per-lane state is reloaded (coalesced) where it is needed rather than
@@ -3464,24 +3478,24 @@ static void launch_push_w(Ctx* c, ExpandArgs a) {
   // the bitmap pays once the push has many arcs (a pass over n vertices
   // against three scattered loads per arc)
   if (lanes && c->push_est * 16.0 >= (double)c->n_alloc) {
-    hipLaunchKernelGGL(k_mkneed, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
+    hipLaunchKernelGGL(k_mkneed, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8 * GS))),
                        dim3(BLOCK), 0, s, c->d_state, c->d_seenpop, c->d_done_at, a.vbegin, a.nloc, c->n_alloc,
                        c->d_nbits);
     a.nbits = c->d_nbits;
   }
   hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_abits, nwords,
                      a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats, (const int64_t*)nullptr, 0);
-  hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
-  hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8 * GS), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4 * GS), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_touch_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, s, c->d_tbits, nwords,
                      c->d_touched, c->d_stats);
   if (lanes)   // a wave per 64 touched receivers at a time, grid-stride
     hipLaunchKernelGGL(k_apply_lanes<W>, dim3(std::max(1, std::min(grid_for(std::max<int64_t>(c->nloc(), 1),
                                                                              (int64_t)WAVES * 64),
-                                                                    c->cu_count * 8))),
+                                                                    c->cu_count * 8 * GS))),
                        dim3(BLOCK), 0, s, a);
   else
-    hipLaunchKernelGGL(k_apply<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, s, a);
+    hipLaunchKernelGGL(k_apply<W>, dim3(c->cu_count * 8 * GS), dim3(BLOCK), 0, s, a);
 }
 
 template <int W>
@@ -3490,13 +3504,13 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     launch_push_w<W>(c, a);
     return;
   }
-  const int64_t per_block = (int64_t)WAVES * 64;
+  const int64_t per_block = (int64_t)EWAVES * 64;   // k_expand
   if (a.unfiltered && c->liveness_active)
-    hipLaunchKernelGGL(k_park<W>, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8)),
+    hipLaunchKernelGGL(k_park<W>, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8 * GS)),
                        dim3(BLOCK), 0, c->stream,
                        c->d_state, c->d_sp, c->d_slot[0], c->d_slot[1], c->d_slot[2], c->n_alloc);
   if (a.unfiltered)
-    hipLaunchKernelGGL(k_fixup_rows<W>, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8)),
+    hipLaunchKernelGGL(k_fixup_rows<W>, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8 * GS)),
                        dim3(BLOCK), 0, c->stream,
                        c->d_abits, c->d_ws, c->d_slot[c->cur], c->cur, c->n_alloc);
   // W = 32 rows take the per-receiver kernel, except in dense near-done rounds
@@ -3534,8 +3548,8 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     hipLaunchKernelGGL(k_active_list, dim3(grid_for(nwords, BLOCK)), dim3(BLOCK), 0, c->stream, c->d_abits, nwords,
                        a.orp, PUSH_CHUNK, c->d_active, c->d_big, c->d_stats, (const int64_t*)c->d_row_ptr,
                        c->cfg.split_deg);
-    hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8), dim3(BLOCK), 0, c->stream, p);
-    hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4), dim3(BLOCK), 0, c->stream, p);
+    hipLaunchKernelGGL(k_push<W>, dim3(c->cu_count * 8 * GS), dim3(BLOCK), 0, c->stream, p);
+    hipLaunchKernelGGL(k_push_big<W>, dim3(c->cu_count * 4 * GS), dim3(BLOCK), 0, c->stream, p);
   }
   (void)hipEventRecord(c->ev[4], c->stream);
   // line masks of the senders' rows (SCAN_LINES; inside the pull's events and bytes)
@@ -3544,18 +3558,18 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
 
   const bool lm_from_commits = lines && a.lm != c->d_lm;
   if (lines && a.lm == c->d_lm)   // (the last round's commits did not write them)
-    hipLaunchKernelGGL(k_mklm, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
+    hipLaunchKernelGGL(k_mklm, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8 * GS))),
                        dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], a.rows, c->n_alloc, c->d_lm, a.partial);
   if (a.nloc > 0 && flat) {   // narrow rows: edge-parallel pull
-    const dim3 grid(grid_for(a.nloc, (int64_t)WAVES * FlatNR<W>::value));
+    const dim3 grid(grid_for(a.nloc, (int64_t)EWAVES * FlatNR<W>::value));
     if constexpr (W <= 32) {
       const bool ee = a.early_exit != 0 && GP_FLAT_EE_PREFIX > 0;
       if (mode == SCAN_UNFILTERED) {
-        if (ee) hipLaunchKernelGGL((k_expand_flat<W, SCAN_UNFILTERED, true>), grid, dim3(BLOCK), 0, c->stream, a);
-        else hipLaunchKernelGGL((k_expand_flat<W, SCAN_UNFILTERED, false>), grid, dim3(BLOCK), 0, c->stream, a);
+        if (ee) hipLaunchKernelGGL((k_expand_flat<W, SCAN_UNFILTERED, true>), grid, dim3(EBLOCK), 0, c->stream, a);
+        else hipLaunchKernelGGL((k_expand_flat<W, SCAN_UNFILTERED, false>), grid, dim3(EBLOCK), 0, c->stream, a);
       } else {
-        if (ee) hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED, true>), grid, dim3(BLOCK), 0, c->stream, a);
-        else hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED, false>), grid, dim3(BLOCK), 0, c->stream, a);
+        if (ee) hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED, true>), grid, dim3(EBLOCK), 0, c->stream, a);
+        else hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED, false>), grid, dim3(EBLOCK), 0, c->stream, a);
       }
     }
   } else if (a.nloc > 0) {
@@ -3564,21 +3578,21 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     if constexpr (W >= 32) alive_ee = mode == SCAN_UNFILTERED && a.alive && a.early_exit;
     if (alive_ee) {
       if constexpr (W >= 32)
-        hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
+        hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE>), grid, dim3(EBLOCK), 0, c->stream, a);
     } else if (mode == SCAN_UNFILTERED) {
-      hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+      hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(EBLOCK), 0, c->stream, a);
     }
     else if (masked)
-      hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(BLOCK), 0, c->stream, a);
+      hipLaunchKernelGGL((k_expand<W, SCAN_MASKED>), grid, dim3(EBLOCK), 0, c->stream, a);
     else if (W == 64 && (a.cmk || a.cmk_next)) {   // compact Message-Lists read and / or written
       if constexpr (W == 64) {
         if (GP_REC_FLAT && a.cmk && !a.early_exit && !c->prefilter_now && !a.alive)
           hipLaunchKernelGGL(k_expand_rec, dim3(grid_for(a.nloc, (int64_t)WAVES * REC_NR)), dim3(BLOCK), 0,
                              c->stream, a);
         else if (c->prefilter_now)
-          hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_CML>), grid, dim3(BLOCK), 0, c->stream, a);
+          hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_CML>), grid, dim3(EBLOCK), 0, c->stream, a);
         else
-          hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_CML>), grid, dim3(BLOCK), 0, c->stream, a);
+          hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_CML>), grid, dim3(EBLOCK), 0, c->stream, a);
       }
     } else {
       // early-exit rounds with alive sets (liveness) take the SCAN_ALIVE
@@ -3588,15 +3602,15 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
       if constexpr (W >= 32) {
         if (a.alive && a.early_exit) {
           if (c->prefilter_now)
-            hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
+            hipLaunchKernelGGL((k_expand<W, SCAN_PRE | SCAN_ALIVE>), grid, dim3(EBLOCK), 0, c->stream, a);
           else
-            hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_ALIVE>), grid, dim3(BLOCK), 0, c->stream, a);
+            hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_ALIVE>), grid, dim3(EBLOCK), 0, c->stream, a);
           done = true;
         }
       }
       if constexpr (W == 64) {
         if (!done && lines) {
-          hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_LINES>), grid, dim3(BLOCK), 0, c->stream, a);
+          hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_LINES>), grid, dim3(EBLOCK), 0, c->stream, a);
           c->lines_ran = true;
           c->lines_from_commits = lm_from_commits;
           done = true;
@@ -3604,9 +3618,9 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
       }
       if (done) {
       } else if (c->prefilter_now)
-        hipLaunchKernelGGL((k_expand<W, SCAN_PRE>), grid, dim3(BLOCK), 0, c->stream, a);
+        hipLaunchKernelGGL((k_expand<W, SCAN_PRE>), grid, dim3(EBLOCK), 0, c->stream, a);
       else
-        hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, a);
+        hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(EBLOCK), 0, c->stream, a);
     }
   }
   if (c->n_hub_items > 0) {
@@ -3625,7 +3639,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   (void)hipEventRecord(c->ev[5], c->stream);
   if (a.prehi) {   // degree-split round: the accumulator back to all-zero
     const int64_t nwords = (c->n_alloc + 63) / 64;
-    hipLaunchKernelGGL(k_acc_clear<W>, dim3(std::max(1, std::min(grid_for(nwords, WAVES), c->cu_count * 8))),
+    hipLaunchKernelGGL(k_acc_clear<W>, dim3(std::max(1, std::min(grid_for(nwords, WAVES), c->cu_count * 8 * GS))),
                        dim3(BLOCK), 0, c->stream, c->d_tbits, c->d_acc, nwords);
   }
 }
@@ -3720,7 +3734,7 @@ static int launch_expand(Ctx* c) {
       !c->local && c->nloc() == c->n_alloc && c->words > c->cfg.flat_max_words && c->sate_since >= 0 &&
       c->round > c->sate_since)
     c->dnb_now = true;
-  hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8))),
+  hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8 * GS))),
                      dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc,
                      c->d_seenpop, c->d_done_at, c->dnb_now ? c->d_dbits : nullptr,
                      c->dnb_now && c->liveness_active ? (const uint8_t*)c->d_state : nullptr);
@@ -3835,7 +3849,7 @@ static int launch_expand(Ctx* c) {
 
 template <int W>
 static void launch_bitsum_w(Ctx* c, BitsumArgs a, bool cnt, bool sum) {
-  const int grid = std::max(1, std::min(grid_for(a.count, (int64_t)WAVES * (64 / W)), c->cu_count * 2));
+  const int grid = std::max(1, std::min(grid_for(a.count, (int64_t)WAVES * (64 / W)), c->cu_count * 2 * GS));
   if (cnt && sum)
     hipLaunchKernelGGL((k_bitsum<W, true, true>), dim3(grid), dim3(BLOCK), 0, c->stream, a);
   else if (cnt)
@@ -4615,18 +4629,18 @@ static int round_launch(Ctx* c) {
     la.p_thresh = (p > 0.0 && p < 1.0) ? (uint64_t)std::ldexp(p, 64) : 0ull;
     la.miss_thr = c->cfg.miss_threshold;
     la.r = r;
-    hipLaunchKernelGGL(k_churn, dim3(std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8)), dim3(BLOCK), 0, s, la);
+    hipLaunchKernelGGL(k_churn, dim3(std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8 * GS)), dim3(BLOCK), 0, s, la);
     la.det_big = c->d_det_big;
     la.det_pre = c->d_det_pre;
     la.det_live = c->d_det_live;
     la.det_cur = c->d_det_cur;
     la.det_base = c->d_det_base;
-    hipLaunchKernelGGL(k_detect, dim3(c->cu_count * GP_DETECT_BLOCKS_PER_CU), dim3(BLOCK), 0, s, la);
+    hipLaunchKernelGGL(k_detect, dim3(c->cu_count * GP_DETECT_BLOCKS_PER_CU * GS), dim3(BLOCK), 0, s, la);
     if (la.det_big) {
       hipLaunchKernelGGL(k_det_big_scan, dim3(1), dim3(1024), 0, s, la);
-      hipLaunchKernelGGL(k_det_big_count, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, la);
+      hipLaunchKernelGGL(k_det_big_count, dim3(c->cu_count * 4 * GS), dim3(BLOCK), 0, s, la);
       hipLaunchKernelGGL(k_det_big_reserve, dim3(DET_CAP / BLOCK), dim3(BLOCK), 0, s, la);
-      hipLaunchKernelGGL(k_det_big_write, dim3(c->cu_count * 4), dim3(BLOCK), 0, s, la);
+      hipLaunchKernelGGL(k_det_big_write, dim3(c->cu_count * 4 * GS), dim3(BLOCK), 0, s, la);
     }
     GP_HIP(hipGetLastError());
     c->pending_crash = false;
