@@ -62,6 +62,12 @@ constexpr int GS = 256 / BLOCK;     // grid-stride kernels' blocks per CU scale:
 #endif
 constexpr int EBLOCK = GP_EXPAND_BLOCK;
 constexpr int EWAVES = EBLOCK / 64;
+// the hub passes the same way (GP_HUB_BLOCK; experiment: 256 = before)
+#ifndef GP_HUB_BLOCK
+#define GP_HUB_BLOCK 256
+#endif
+constexpr int HBLOCK = GP_HUB_BLOCK;
+constexpr int HWAVES = HBLOCK / 64;
 constexpr int NPART = 2048;        // partial stat slots (spread the atomics)
 
 // ---------------------------------------------------------------------------
@@ -1968,15 +1974,15 @@ __global__ __launch_bounds__(BLOCK) void k_expand_rec(ExpandArgs a) {
 
 // hubs, pass 1: one wave per (hub, arc chunk) -> partial OR row
 template <int W, int MODE>
-__global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
+__global__ __launch_bounds__(HBLOCK) void k_hub_partial(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
-  __shared__ WaveLds s_w[WAVES];
+  __shared__ WaveLds s_w[HWAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
   WaveStats st;
   ws_zero(st);
-  const int64_t it = (int64_t)blockIdx.x * WAVES + wib;
+  const int64_t it = (int64_t)blockIdx.x * HWAVES + wib;
   if (it < a.n_items) {
     const HubItem h = a.hub_items[it];
     const int64_t i = h.v - a.vbegin;
@@ -1997,15 +2003,15 @@ __global__ __launch_bounds__(BLOCK) void k_hub_partial(ExpandArgs a) {
 
 // hubs, pass 2: one wave per hub -> OR the partials, then the receiver side
 template <int W>
-__global__ __launch_bounds__(BLOCK) void k_hub_final(ExpandArgs a) {
+__global__ __launch_bounds__(HBLOCK) void k_hub_final(ExpandArgs a) {
   constexpr int LPR = Geo<W>::LPR;
-  __shared__ WaveLds s_w[WAVES];
+  __shared__ WaveLds s_w[HWAVES];
   const int lane = threadIdx.x & 63;
   const int wib = uniform(threadIdx.x >> 6);
   const int g = lane / LPR, lw = lane % LPR;
   WaveStats st;
   ws_zero(st);
-  const int64_t h = (int64_t)blockIdx.x * WAVES + wib;
+  const int64_t h = (int64_t)blockIdx.x * HWAVES + wib;
   alive_zero<W>(a, s_w[wib].alive, lane);
   wave_sync_lds();
   if (h < a.n_items) {
@@ -3626,13 +3632,13 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
   if (c->n_hub_items > 0) {
     ExpandArgs h = a;
     h.n_items = c->n_hub_items;
-    const dim3 grid(grid_for(h.n_items, WAVES));
+    const dim3 grid(grid_for(h.n_items, HWAVES));
     if (mode == SCAN_UNFILTERED)
-      hipLaunchKernelGGL((k_hub_partial<W, SCAN_UNFILTERED>), grid, dim3(BLOCK), 0, c->stream, h);
+      hipLaunchKernelGGL((k_hub_partial<W, SCAN_UNFILTERED>), grid, dim3(HBLOCK), 0, c->stream, h);
     else
-      hipLaunchKernelGGL((k_hub_partial<W, SCAN_FILTERED>), grid, dim3(BLOCK), 0, c->stream, h);
+      hipLaunchKernelGGL((k_hub_partial<W, SCAN_FILTERED>), grid, dim3(HBLOCK), 0, c->stream, h);
     h.n_items = c->n_hubs;
-    hipLaunchKernelGGL(k_hub_final<W>, dim3(grid_for(h.n_items, WAVES)), dim3(BLOCK), 0, c->stream, h);
+    hipLaunchKernelGGL(k_hub_final<W>, dim3(grid_for(h.n_items, HWAVES)), dim3(HBLOCK), 0, c->stream, h);
   }
   // kernel_ms brackets the pull kernel and the hub passes: the round's
   // counters (row bytes, arcs scanned, rows written) include the hubs' share
