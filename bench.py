@@ -122,6 +122,30 @@ def round_bytes(st, words, nloc):
             + (w8 + 23) * st["rows_written"] + w8 * st.get("lm_rows", 0))
 
 
+def message_table(origin, nranks, assign, order, message_shard):
+    """The message table of a run in spread order (order(o) -> permutation of
+    o, fastest first).  One rank: the whole table ordered.  nranks message
+    shards (rank p takes message_shard(m, nranks, p), word-aligned blocks):
+    blocked -- the whole table ordered, then cut (each rank's messages spread
+    at one speed); interleaved -- each rank's block of the drawn table ordered
+    inside; wordsnake -- the ordered table's 64-message words dealt to the
+    ranks in snake order.  Always a permutation of origin."""
+    m = len(origin)
+    if nranks > 1 and assign == "interleaved":
+        blocks = [message_shard(m, nranks, p) for p in range(nranks)]
+    else:
+        blocks = [(0, m)]
+    out = np.concatenate([origin[lo:hi][order(origin[lo:hi])] for lo, hi in blocks])
+    if nranks > 1 and assign == "wordsnake":   # word k of the ordered table to rank snake(k)
+        words = [out[64 * k:64 * (k + 1)] for k in range((m + 63) // 64)]
+        per = [[] for _ in range(nranks)]
+        for k, w in enumerate(words):
+            r, lap = k % nranks, k // nranks
+            per[r if lap % 2 == 0 else nranks - 1 - r].append(w)
+        out = np.concatenate([np.concatenate(x) for x in per if x])
+    return out
+
+
 def engine_config(args):
     """The engine configuration of the timed run (tests/test_full_size.py
     checks a run configured by this very function against the oracle)."""
@@ -273,17 +297,8 @@ def main():
         # messages spread at one speed and its receivers complete together (the
         # N = 8 job's slowest rank 22.3 -> 13.4 ms against interleaved: within
         # each rank's block of the drawn table); DESIGN.md §6
-        blocks = ([dist.message_shard(args.messages, s_world, p) for p in range(s_world)]
-                  if shards and args.shard_assign == "interleaved" else [(0, args.messages)])
-        origin = np.concatenate([origin[lo:hi][eng.spread_order(origin[lo:hi], hops=args.spread_hops)]
-                                 for lo, hi in blocks])
-        if shards and args.shard_assign == "wordsnake":   # word k of the ordered table to rank snake(k)
-            words = [origin[64 * k:64 * (k + 1)] for k in range((args.messages + 63) // 64)]
-            per = [[] for _ in range(s_world)]
-            for k, w in enumerate(words):
-                r, lap = k % s_world, k // s_world
-                per[r if lap % 2 == 0 else s_world - 1 - r].append(w)
-            origin = np.concatenate([np.concatenate(x) for x in per if x])
+        origin = message_table(origin, s_world if shards else 1, args.shard_assign,
+                               lambda o: eng.spread_order(o, hops=args.spread_hops), dist.message_shard)
     if world > 1 and not shards:
         eng.set_partition(rank, world)
         eng.comm_init(dist.share_comm_id(pg, pkg.GossipEngine.comm_unique_id), world, rank)
