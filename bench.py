@@ -70,7 +70,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-log2n", type=int, default=None,
                     help="cpu_baseline: overlay size of the oracle's run (all messages, W = 64); default: the "
-                         "workload's own size up to 2^24 -- the whole C4 run, ~30 s on 16 host threads")
+                         "workload's own size -- the whole C4 run (~30 s on 16 host threads), or the whole C5 "
+                         "run with churn (2^26, ~100 s and ~100 GiB of host memory)")
     ap.add_argument("--parallel", choices=("messages", "vertex"), default="messages",
                     help="N > 1: message shards (no data-path collective, default) or the vertex "
                          "partition with a sparse boundary exchange every round (ncclSend/Recv of "
@@ -90,8 +91,8 @@ def parse(argv=None):
     c5 = a.workload == "c5"
     if a.log2n is None:
         a.log2n = 26 if c5 else 24
-    if a.cpu_log2n is None:   # C4 itself; C5's 2^26 (4x the rows and arcs) is sampled at 2^24
-        a.cpu_log2n = min(a.log2n, 24)
+    if a.cpu_log2n is None:   # the workload itself: C4, or C5 with churn at 2^26
+        a.cpu_log2n = a.log2n
     if a.seed is None:
         a.seed = 5 if c5 else 4
     return a
@@ -111,15 +112,18 @@ def round_bytes(st, words, nloc):
     slot 8W B; plus the senders' rows read to build line masks (k_mklm, 8W B
     each) before a filtered 64-word pull."""
     w8 = 8 * words
-    scan = st.get("scan", 0)
+    scan = st.get("scan", 0) & 3
     if scan == 2:
         arcs = 4 * st["arcs_scanned"]
     elif scan == 1:
         arcs = st["arcs_scanned"] / 8 + 4 * st["rows_gathered"] + 8 * nloc
     else:
         arcs = 12 * st["arcs_scanned"]
+    # degree-split rounds (scan bit 32): the push half's accumulator updates,
+    # 8 B each (kernel_ms brackets the push half and the clear too)
+    split = 8 * st.get("atomics", 0) if st.get("scan", 0) & 32 else 0
     return (30 * nloc + arcs + st["row_bytes"] + w8 * st["seen_rows_read"]
-            + (w8 + 23) * st["rows_written"] + w8 * st.get("lm_rows", 0))
+            + (w8 + 23) * st["rows_written"] + w8 * st.get("lm_rows", 0) + split)
 
 
 def message_table(origin, nranks, assign, order, message_shard):
@@ -131,6 +135,11 @@ def message_table(origin, nranks, assign, order, message_shard):
     inside; wordsnake -- the ordered table's 64-message words dealt to the
     ranks in snake order.  Always a permutation of origin."""
     m = len(origin)
+    nwords = (m + 63) // 64
+    if nranks > 1 and assign == "wordsnake" and nwords % nranks:
+        # (snake order deals equal word counts; the shard blocks would cut
+        # unequal ones, handing ranks part of a neighbour's words)
+        raise ValueError(f"wordsnake needs the {nwords} words to divide among {nranks} ranks")
     if nranks > 1 and assign == "interleaved":
         blocks = [message_shard(m, nranks, p) for p in range(nranks)]
     else:
@@ -211,9 +220,10 @@ def cpu_baseline(args, eng, origin, pkg):
                use: OMP_NUM_THREADS, else the affinity set) running ALL
                `messages` (W = 64 words per Message-List row, the GPU's layout)
                to quiescence on a 2^cpu_log2n-vertex overlay of the same
-               Chung-Lu recipe and seed: by default the workload itself at
-               C4 (the same overlay the GPU ran, 2^24 x 4096: ~30 s on 16
-               threads), a 2^24 sample of C5; this leg is `value`;
+               Chung-Lu recipe and seed: by default the workload itself, on
+               the overlay the GPU ran (C4 2^24 x 4096: ~30 s on 16 threads;
+               C5 2^26 x 4096 with churn, the same crash stream: ~100 s);
+               this leg is `value`;
       harness  oracle/harness.py, the reference's per-peer Message-List logic
                (sha256 digests in a set per peer, Peer.py:175-216, 395-408) plus
                forwarding, single-core, on BASELINE config 2 (10^4-node BA(m=2),

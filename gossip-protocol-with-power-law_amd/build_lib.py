@@ -12,8 +12,9 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 OUT_DIR = os.path.join(PKG_DIR, "_build")
 LIB = os.path.join(OUT_DIR, "libgossip_hip.so")
 INCLUDE = os.path.join(os.path.dirname(PKG_DIR), "include", "gossip_capi.h")
-SOURCES = ["gossip_engine.hip", "graph_build.hip", "checkpoint.hip", "partition.hip", "bitcount.hip"]
-HEADERS = ["gp_common.h", "gp_internal.h", "xplan.h"]
+SOURCES = ["driver.hip", "setup.hip", "pull.hip", "hub.hip", "push.hip", "liveness.hip", "graph_build.hip",
+           "checkpoint.hip", "partition.hip", "bitcount.hip"]
+HEADERS = ["gp_common.h", "gp_internal.h", "gp_device.h", "xplan.h"]
 ARCH = os.environ.get("GOSSIP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", f"--offload-arch={ARCH}"]
 
@@ -47,7 +48,7 @@ def build_standin(force=False, verbose=True):
     if not force and not _stale(STANDIN_LIB, objs + [STANDIN_SRC, __file__]):
         return STANDIN_LIB
     sobj = os.path.join(OUT_DIR, "rccl_standin.o")
-    cmd = [_hipcc(), "-O2", "-std=c++17", "-fPIC", "-Wall", "-c", STANDIN_SRC, "-o", sobj]
+    cmd = [_hipcc(), "-O2", "-std=c++17", "-fPIC", "-Wall", f"--offload-arch={ARCH}", "-c", STANDIN_SRC, "-o", sobj]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)

@@ -394,12 +394,9 @@ static int bc_keys(Ctx* c) {
   return 0;
 }
 
-#ifndef GP_BC_LIN
-#define GP_BC_LIN 1
-#endif
 template <int W>
 static void launch_bitcount_w(Ctx* c, BitcountArgs a, bool weighted, int nblocks) {
-  if (GP_BC_LIN && W == 64 && !weighted)   // (grid: nblocks, sized by the caller to the resident blocks)
+  if (W == 64 && !weighted)   // (grid: nblocks, sized by the caller to the resident blocks)
     hipLaunchKernelGGL(k_bitcount_lin, dim3(nblocks), dim3(BC_BLOCK), 0, c->stream, a);
   else if (weighted)
     hipLaunchKernelGGL((k_bitcount<W, true>), dim3(nblocks), dim3(BC_BLOCK), 0, c->stream, a);
@@ -419,7 +416,7 @@ int bitcount_messages(Ctx* c, bool weighted, u64* cov, u64* fwd) {
   if (weighted) n = c->bc_split;   // the tail is counted by k_bitcount_tail
   const int64_t rows_per_block = (int64_t)BC_WAVES * 512;
   int64_t cap = (int64_t)c->cu_count * 8;
-  if (GP_BC_LIN && W == 64 && !weighted) {   // one wave of resident blocks: equal chunks leave no tail
+  if (W == 64 && !weighted) {   // one wave of resident blocks: equal chunks leave no tail
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bitcount_lin, BC_BLOCK, 0) == hipSuccess &&
         per_cu > 0)

@@ -20,7 +20,7 @@
 namespace gp {
 
 constexpr uint64_t CKPT_MAGIC = 0x3130545048434b47ull;   // "GKCHPT01"
-constexpr uint8_t CK_SLOT_NONE = 0xFF;                   // gossip_engine.hip SLOT_NONE
+constexpr uint8_t CK_SLOT_NONE = 0xFF;                   // gp_device.h SLOT_NONE
 constexpr int64_t CK_CHUNK_WORDS = (int64_t)8 << 20;     // 64 MB of rows per staging pass
 
 struct CkptHeader {
@@ -30,7 +30,7 @@ struct CkptHeader {
   int32_t m, msg_word_base;
   int32_t round, cur;
   int32_t liveness_active, pending_crash, msg_forwards_valid, done_dirty;
-  int32_t has_first, has_frx, cmask_rows, reserved;
+  int32_t has_first, has_frx, cmask_rows, alive_from1;   // alive_from + 1 (0: no complete alive set)
   uint64_t prev_next_arcs, prev_new_bits, prev_receivers, held_bits;
   int64_t last_reports;     // reports of the round just taken (exact count)
   int64_t saved_reports;    // how many of them the blob holds (<= the report buffer)
@@ -129,6 +129,7 @@ int gp_checkpoint_save(gp_ctx* c, void* host, int64_t bytes) {
   h.has_first = c->d_first && c->cfg.track_first ? 1 : 0;
   h.has_frx = c->d_frx[0] ? 1 : 0;
   h.cmask_rows = c->cmask_rows;
+  h.alive_from1 = c->alive_from + 1;
   h.prev_next_arcs = c->prev_next_arcs; h.prev_new_bits = c->prev_new_bits;
   h.prev_receivers = c->prev_receivers; h.held_bits = c->held_bits;
   h.last_reports = c->last_reports;
@@ -225,6 +226,7 @@ int gp_checkpoint_load(gp_ctx* c, const void* host, int64_t bytes) {
     GP_TRY(copy_sync(c, c->d_ws, ws.data(), na, hipMemcpyHostToDevice));
   }
   c->liveness_active = h.liveness_active != 0;
+  c->alive_from = h.alive_from1 - 1;
   c->pending_crash = h.pending_crash != 0;
   c->msg_forwards_valid = h.msg_forwards_valid != 0;
   c->done_dirty = true;   // the working targets came from the blob; the next reset restores the pristine ones

@@ -27,8 +27,12 @@ enum StatSlot {
   S_DNB,               // receivers completed from a done in-neighbour (k_expand)
   S_LM_ROWS,           // senders' rows read by k_mklm to build line masks
   NST,
+  // boundary entries the unpack found inconsistent with the exchange plan
+  // (partition.hip k_rx_unpack); all-reduced with the counters, fails the round
+  S_XERR = NST + 1,
   S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR, S_DET_BIG
 };
+static_assert(S_XERR < S_REPORT_CURSOR, "S_XERR must be inside the all-reduced counter slots");
 
 struct HubItem {       // one wave's share of a hub's in-list
   int32_t v;           // hub vertex
@@ -117,6 +121,7 @@ struct Ctx {
   // Message-List slots: v's seen row lives in d_slot[d_sp[v]];
   // round r reads S[r & 1] and writes S[(r + 1) & 1]; cur == r & 1
   u64* d_slot[3] = {nullptr, nullptr, nullptr};    // [n_alloc][W]; slot 2: parked rows (below)
+  u64* d_rows = nullptr;            // the allocation of d_slot[0], d_slot[1] and d_acc (in that order)
   // parking: an unfiltered pull under liveness reads every in-neighbour's row
   // of slot r & 1, so before it the rows of down vertices move to slot 2
   // (sp = 2) and both read-slot rows are zeroed; slot 2 is allocated lazily
@@ -143,7 +148,7 @@ struct Ctx {
   double push_est = 0.0;            // sender arcs the direction estimate saw this round
   u64* d_nbits = nullptr;           // [n_alloc/64] narrow push rounds: receivable vertices (k_mkneed)
   u64* d_abits = nullptr;
-  u64* d_sbits = nullptr;   // summary level of d_abits (GP_SUMMARY_PROBE builds)
+  u64* d_sbits = nullptr;   // summary level of d_abits (summary probes)
   // [n_alloc/64] done bitmap of early-exit rounds without liveness (single
   // context): bit v = v held every message of its component at the end of the
   // last round (done in-neighbours)
@@ -169,7 +174,7 @@ struct Ctx {
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
   u64* d_amask = nullptr;
   // push (sparse-round) mode
-  u64* d_acc = nullptr;             // [n_alloc][W] OR accumulator, kept all-zero between uses
+  u64* d_acc = nullptr;             // [nloc][W] OR accumulator, kept all-zero between uses (inside d_rows)
   u64* d_tbits = nullptr;           // [n_alloc/64] receivers pushed to this round
   int32_t* d_touched = nullptr;     // [n_alloc] receivers touched this round
   int32_t* d_active = nullptr;      // [n_alloc] senders (deg <= hub threshold)
@@ -183,7 +188,7 @@ struct Ctx {
   u64 held_bits = 0;                // messages held so far, summed over vertices (global)
   bool unfiltered_now = false;      // this round's pull skips the activity check
   bool arc_mask_now = false;        // this round's filtered pull reads the per-arc mask
-  bool sum_now = false;             // this round's probes read the summary level first (GP_SUMMARY_PROBE)
+  bool sum_now = false;             // this round's probes read the summary level first
   bool prefilter_now = false;       // this round's filtered pull probes low-degree in-lists lane-parallel
   // compact Message-Lists: 128-B records per vertex, per slot
   u64* d_cml[2] = {nullptr, nullptr};   // [n_alloc][16] records
@@ -227,6 +232,11 @@ struct Ctx {
   u64* h_stats = nullptr;      // pinned [NSTAT]
   int32_t round = 0;
   bool liveness_active = false;
+  // first round whose alive set F_r is complete in d_alive (-1: none yet).
+  // The sets are built only while liveness is active, so when an explicit
+  // crash turns it on at round r, F_r was never built: r's pull must not
+  // narrow its early-exit target with it (F_{r+1} is built by round r)
+  int32_t alive_from = -1;
   bool pending_crash = false;
   bool msg_forwards_valid = true;
   int64_t last_reports = 0;
@@ -295,7 +305,7 @@ int copy_sync(Ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind ki
 int build_chung_lu(Ctx* c, int64_t n, double dbar, double gamma, uint64_t seed);
 int build_gather_order(Ctx* c);
 int build_prehi(Ctx* c, int32_t T);
-// gossip_engine.hip
+// setup.hip
 int finish_graph(Ctx* c);
 int build_hubs(Ctx* c);
 // bitcount.hip

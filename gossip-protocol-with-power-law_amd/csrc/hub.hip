@@ -1,0 +1,93 @@
+// hub.hip -- hub receivers of the pull (hub load balancing):
+// vertices above hub_threshold in-arcs are split over waves, each wave ORs one
+// chunk of the in-list into a partial row (k_hub_partial), k_hub_final combines
+// a hub's partials and commits the row.  Deterministic, no atomics on rows.
+#include "gp_device.h"
+
+namespace gp {
+
+// hubs, pass 1: one wave per (hub, arc chunk) -> partial OR row
+template <int W, int MODE>
+__global__ __launch_bounds__(HBLOCK) void k_hub_partial(ExpandArgs a) {
+  constexpr int LPR = Geo<W>::LPR;
+  __shared__ WaveLds s_w[HWAVES];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  WaveStats st;
+  ws_zero(st);
+  const int64_t it = (int64_t)blockIdx.x * HWAVES + wib;
+  if (it < a.n_items) {
+    const HubItem h = a.hub_items[it];
+    const int64_t i = h.v - a.vbegin;
+    u64x2 acc = {0, 0};
+    if (!(a.state[h.v] & (ST_DOWN | ST_SATED)) && a.seenpop[i] < a.done_at[h.v]) {
+      const bool ee = a.early_exit != 0;
+      u64x2 want = {0, 0};
+      if (ee) want = early_exit_target<W>(a, h.v, s_w[wib], g, lw, a.sp[h.v], a.midx[h.v]);
+      gather_scan<W, MODE>(a, h.beg, h.end, s_w[wib], lane, g, lw, acc, st, ee, want);
+      reduce_slots<W>(acc);
+    }
+    const bool nz = __any((acc.x | acc.y) != 0);
+    if (nz && g == 0) store_piece<W>(a.hub_partial, it, lw, acc);
+    if (lane == 0) a.hub_pnz[it] = nz ? 1u : 0u;
+  }
+  flush_stats(st, a.partial);
+}
+
+// hubs, pass 2: one wave per hub -> OR the partials, then the receiver side
+template <int W>
+__global__ __launch_bounds__(HBLOCK) void k_hub_final(ExpandArgs a) {
+  constexpr int LPR = Geo<W>::LPR;
+  __shared__ WaveLds s_w[HWAVES];
+  const int lane = threadIdx.x & 63;
+  const int wib = uniform(threadIdx.x >> 6);
+  const int g = lane / LPR, lw = lane % LPR;
+  WaveStats st;
+  ws_zero(st);
+  const int64_t h = (int64_t)blockIdx.x * HWAVES + wib;
+  alive_zero<W>(a, s_w[wib].alive, lane);
+  wave_sync_lds();
+  if (h < a.n_items) {
+    const int v = a.hubs[h];
+    const int64_t i = v - a.vbegin;
+    if ((a.state[v] & (ST_DOWN | ST_SATED)) || a.seenpop[i] >= a.done_at[v]) {
+      if (lane == 0) a.fpop_next[v] = 0;
+    } else {
+      st.add(S_VISITED, 1);
+      u64x2 acc = {0, 0};
+      const int p0 = a.hub_item_ptr[h], p1 = a.hub_item_ptr[h + 1];
+      if (g == 0) {
+        for (int p = p0; p < p1; ++p)
+          if (a.hub_pnz[p]) acc |= load_piece<W>(a.hub_partial, p, lw);
+        if (a.prehi) acc |= load_piece<W>(a.acc, v, lw);   // degree-split round: the push half's OR (k_acc_clear zeroes it)
+      }
+      finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
+    }
+  }
+  alive_flush<W>(a, s_w[wib].alive, lane);
+  flush_stats(st, a.partial);
+}
+
+
+template <int W>
+void launch_hubs_w(Ctx* c, const ExpandArgs& a, bool unfiltered) {
+  ExpandArgs h = a;
+  h.n_items = c->n_hub_items;
+  const dim3 grid(grid_for(h.n_items, HWAVES));
+  if (unfiltered)
+    hipLaunchKernelGGL((k_hub_partial<W, SCAN_UNFILTERED>), grid, dim3(HBLOCK), 0, c->stream, h);
+  else
+    hipLaunchKernelGGL((k_hub_partial<W, SCAN_FILTERED>), grid, dim3(HBLOCK), 0, c->stream, h);
+  h.n_items = c->n_hubs;
+  hipLaunchKernelGGL(k_hub_final<W>, dim3(grid_for(h.n_items, HWAVES)), dim3(HBLOCK), 0, c->stream, h);
+}
+template void launch_hubs_w<1>(Ctx*, const ExpandArgs&, bool);
+template void launch_hubs_w<2>(Ctx*, const ExpandArgs&, bool);
+template void launch_hubs_w<4>(Ctx*, const ExpandArgs&, bool);
+template void launch_hubs_w<8>(Ctx*, const ExpandArgs&, bool);
+template void launch_hubs_w<16>(Ctx*, const ExpandArgs&, bool);
+template void launch_hubs_w<32>(Ctx*, const ExpandArgs&, bool);
+template void launch_hubs_w<64>(Ctx*, const ExpandArgs&, bool);
+
+}  // namespace gp

@@ -406,6 +406,14 @@ __global__ __launch_bounds__(PBLOCK) void k_rx_size(const u64* __restrict__ rh, 
   out[h] = h < nh ? 1ull + (rh[h] >> 40) : 0ull;
 }
 
+// Received entries are checked against the exchange plan before anything is
+// written (a transfer that does not match it must fail loudly on every rank,
+// not write out of bounds): the entry's ghost index lies within the ghosts of
+// its sender, its flags are a new row and / or a removal, its word count is
+// the popcount of its mask (which names only the row's W words), and the
+// heads' word counts add up to the words the plan received.  Each bad entry
+// adds 1 to stats[S_XERR], which the counters' all-reduce carries to every
+// rank (round_collect turns it into GP_ERCCL).
 __global__ __launch_bounds__(PBLOCK) void k_rx_unpack(const u64* __restrict__ rh, const u64* __restrict__ rw,
                                                       const u64* __restrict__ rscan, int64_t nh, PeerTable pt,
                                                       int32_t P, int64_t nloc, int32_t W, int32_t nx,
@@ -413,17 +421,28 @@ __global__ __launch_bounds__(PBLOCK) void k_rx_unpack(const u64* __restrict__ rh
                                                       uint8_t* __restrict__ sp, uint8_t* __restrict__ ws,
                                                       uint8_t* __restrict__ state, int32_t* __restrict__ deg_live,
                                                       const int64_t* __restrict__ row_ptr,
-                                                      const int32_t* __restrict__ col) {
+                                                      const int32_t* __restrict__ col, u64 words_expected,
+                                                      u64* __restrict__ xerr) {
   const int lane = threadIdx.x & 63;
   const int64_t h = (int64_t)blockIdx.x * PWAVES + (threadIdx.x >> 6);
+  if (h == 0 && lane == 0 && rscan[nh] != words_expected) atomicAdd(xerr, 1ull);
   if (h >= nh) return;
   const u64 head = rh[h];
   int q = 0;
   while (q + 1 < P && (int64_t)pt.rk[q + 1] <= h) ++q;
-  const int64_t g = nloc + pt.gh[q] + (int64_t)(uint32_t)head;
+  const uint32_t idx = (uint32_t)head;
   const uint32_t f = (uint32_t)(head >> 32) & 0xFFu;
   const u64 woff = rscan[h];
-  const u64 mask = rw[woff];
+  const u64 nwords = head >> 40;
+  bool ok = idx < (uint32_t)(pt.gh[q + 1] - pt.gh[q]) && f >= 1u && f <= 3u && (u64)W <= 64 &&
+            woff + 1 + nwords <= words_expected;
+  const u64 mask = ok ? rw[woff] : 0ull;
+  ok = ok && (u64)__popcll(mask) == nwords && (W == 64 || (mask >> W) == 0ull);
+  if (!ok) {
+    if (lane == 0) atomicAdd(xerr, 1ull);
+    return;
+  }
+  const int64_t g = nloc + pt.gh[q] + (int64_t)idx;
   if (f & 1u) {
     u64 x = 0;
     if (lane < W && ((mask >> lane) & 1ull)) x = rw[woff + 1 + (u64)__popcll(mask & ((1ull << lane) - 1ull))];
@@ -458,7 +477,7 @@ __global__ void k_or_alive(const u64* __restrict__ all, int32_t P, int32_t W, u6
 }
 
 // received heads / words are in place (by sender rank); rk = head prefix per sender
-static int unpack_received(Ctx* c, const std::vector<int64_t>& rk) {
+static int unpack_received(Ctx* c, const std::vector<int64_t>& rk, int64_t rw) {
   hipStream_t s = c->stream;
   const int nx = c->cur ^ 1;
   const int64_t nl = c->nloc(), P = c->nranks;
@@ -470,14 +489,15 @@ static int unpack_received(Ctx* c, const std::vector<int64_t>& rk) {
   hipLaunchKernelGGL(k_rx_size, dim3((unsigned)((nh + 1 + PBLOCK - 1) / PBLOCK)), dim3(PBLOCK), 0, s, c->d_rbuf_h, nh,
                      c->d_xsize);
   GP_TRY(scan_u64(c, c->d_xsize, c->d_rscan, (size_t)nh + 1));
-  PeerTable pt{};
+  PeerTable pt{};   // (P <= MAX_PARTS: checked by localize)
   for (int64_t q = 0; q <= P; ++q) {
     pt.rk[q] = (int32_t)rk[(size_t)q];
     pt.gh[q] = (int32_t)c->h_gh_ptr[(size_t)q];
   }
   hipLaunchKernelGGL(k_rx_unpack, dim3((unsigned)((nh + PWAVES - 1) / PWAVES)), dim3(PBLOCK), 0, s, c->d_rbuf_h,
                      c->d_rbuf_w, c->d_rscan, nh, pt, (int32_t)P, nl, c->words, nx, c->d_slot[nx], c->d_fpop[nx],
-                     c->d_sp, c->d_ws, c->d_state, c->d_deg_live, c->d_row_ptr, c->d_col);
+                     c->d_sp, c->d_ws, c->d_state, c->d_deg_live, c->d_row_ptr, c->d_col, (u64)rw,
+                     c->d_stats + S_XERR);
   GP_HIP(hipGetLastError());
   return 0;
 }
@@ -539,7 +559,6 @@ int exchange_rccl(Ctx* c) {
   GP_TRY(pack_boundary(c));
   u64* alive_next = c->d_alive + (size_t)(c->cur ^ 1) * W;
   GP_RCCL(ncclGroupStart());
-  GP_RCCL(ncclAllReduce(c->d_stats, c->d_stats, S_REPORT_CURSOR, ncclUint64, ncclSum, c->comm, s));
   GP_RCCL(ncclAllGather(c->d_cnt, c->d_cnt_all, 4 * (size_t)P, ncclUint64, c->comm, s));
   if (alive_reduce_on(c)) GP_RCCL(ncclAllGather(alive_next, c->d_alive_all, W, ncclUint64, c->comm, s));
   GP_RCCL(ncclGroupEnd());
@@ -568,7 +587,11 @@ int exchange_rccl(Ctx* c) {
     }
   }
   GP_RCCL(ncclGroupEnd());
-  return unpack_received(c, plan.rk);
+  GP_TRY(unpack_received(c, plan.rk, plan.rw.back()));
+  // the counters' all-reduce after the unpack: it carries the unpack's entry
+  // check (S_XERR) to every rank, so all ranks fail the round together
+  GP_RCCL(ncclAllReduce(c->d_stats, c->d_stats, S_REPORT_CURSOR, ncclUint64, ncclSum, c->comm, s));
+  return 0;
 }
 
 int exchange_group(Ctx** ctxs, int32_t P) {
@@ -618,7 +641,7 @@ int exchange_group(Ctx** ctxs, int32_t P) {
       GP_HIP(hipMemcpyAsync(dst->d_rbuf_w + in.w0, ctxs[q]->d_sbuf_w + out.w0, (size_t)in.nw * 8, hipMemcpyDefault,
                             dst->stream));
     }
-    GP_TRY(unpack_received(dst, plan.rk));
+    GP_TRY(unpack_received(dst, plan.rk, plan.rw.back()));
   }
   return 0;
 }

@@ -88,11 +88,15 @@ typedef struct gp_round_stats {
                                + 4: senders gathered from compact Message-Lists;
                                + 8: 64-word line masks read (only named 128-B lines
                                gathered, §3.2); + 16: those masks were written by
-                               the previous round's commits (no k_mklm pass)       */
+                               the previous round's commits (no k_mklm pass);
+                               + 32: degree-split round (senders of in-degree <
+                               split_deg pushed, receivers probe the gather-order
+                               prefix of the others, §3.2)                        */
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
-  double kernel_ms;         /* device time of the pull kernel + its hub passes       */
+  double kernel_ms;         /* device time of the pull kernel + its hub passes (and
+                               of a degree-split round's push half and clear)    */
   uint64_t xchg_rows;       /* vertex partition: boundary entries sent (all peers)   */
   uint64_t xchg_bytes;      /* vertex partition: bytes sent (entry heads + words)    */
   uint64_t done_nb;         /* receivers that took every message of their component

@@ -9,15 +9,25 @@
 //
 // Model: the P ranks are P threads of one process driving P contexts on one
 // device (tests/rccl_standin_driver.py).  A communicator is a rank of a
-// "world" named by the unique id.  Every call first synchronizes the caller's
-// stream (so the inputs the engine enqueued are in memory), then runs the
-// collective synchronously with the other ranks' threads: barriers order the
-// reads of every rank's inputs before any rank writes its outputs (in-place
-// all-reduce), and point-to-point receives copy straight from the matching
-// sender's buffer (the k-th receive from q matches q's k-th send to this rank
-// inside one group, as in RCCL).  Calls between ncclGroupStart / ncclGroupEnd
-// are recorded and run at the outermost ncclGroupEnd.  Barrier waits time out
-// (ncclSystemError) instead of hanging a test when a rank fails.
+// "world" named by the unique id.  Calls between ncclGroupStart /
+// ncclGroupEnd are recorded and run at the outermost ncclGroupEnd; the k-th
+// receive from q matches q's k-th send to this rank inside one group, as in
+// RCCL.  Barrier waits time out (ncclSystemError) instead of hanging a test
+// when a rank fails.  Two modes (GP_STANDIN_ASYNC in the environment):
+//   sync (default)  every call first synchronizes the caller's stream (so the
+//                   inputs the engine enqueued are in memory), then runs the
+//                   collective with the other ranks' threads and waits for it;
+//   async (=1)      nothing is synchronized: like RCCL, a call only enqueues.
+//                   The copies run on a side stream of each rank that waits on
+//                   an event recorded on the caller's stream at the call, and
+//                   the caller's stream waits on the copies' events (outputs
+//                   landed, send buffers free) before its next work.  An engine
+//                   that wrote an input after the call, or read an output
+//                   without ordering on its stream, sees stale data here.
+// Fault injection (GP_STANDIN_CORRUPT=rank:k): rank `rank` overwrites the
+// first 8 bytes of its k-th non-empty receive (counted from 0 over the
+// communicator's life) with ones, after the copy -- the engine's exchange check
+// must then fail the round on every rank.
 //
 // Built by build_lib.build_standin() into _build/libgossip_hip_rccl_standin.so
 // together with the engine's own objects; the product library links real RCCL.
@@ -26,6 +36,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -49,10 +60,15 @@ struct Op {
   hipStream_t stream;
 };
 
-struct Mail {   // a posted send: the receiver copies from src and sets *done
+struct SendRec {   // the sender's side of a posted send
+  char done = 0;                  // the receiver took it
+  hipEvent_t copied = nullptr;    // async: recorded on the receiver's side stream after its copy
+};
+struct Mail {   // a posted send: the receiver copies from src and sets rec->done
   const void* src;
   size_t bytes;
-  char* done;
+  SendRec* rec;
+  hipEvent_t ready;               // async: the sender's stream reached the send
 };
 
 struct World {
@@ -64,6 +80,8 @@ struct World {
   int arrived = 0;
   bool broken = false;   // a wait timed out: every later wait fails at once
   std::vector<std::vector<Op>*> posted;   // each rank's collectives of the current call
+  std::vector<hipEvent_t> ev;             // async: each rank's published event of the current phase
+  std::vector<void*> stage;               // async: each rank's staged all-reduce input
   std::map<std::pair<int, int>, std::deque<Mail>> box;   // (from, to) -> sends in posting order
 };
 
@@ -82,11 +100,55 @@ thread_local RankState t_rank;
 struct ncclComm {
   World* w;
   int rank;
+  hipStream_t side = nullptr;   // async mode: the stream the copies run on
+  void* stage = nullptr;        // async mode: staged all-reduce input
+  size_t stage_bytes = 0;
+  long recvs = 0;               // non-empty receives so far (fault injection)
 };
 
 namespace {
 
 constexpr int kBarrierTimeoutS = 120;
+
+bool async_mode() {
+  static const bool on = [] {
+    const char* e = std::getenv("GP_STANDIN_ASYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// GP_STANDIN_CORRUPT=rank:k -> (rank, k); (-1, -1) when unset
+std::pair<int, long> corrupt_target() {
+  static const std::pair<int, long> t = [] {
+    const char* e = std::getenv("GP_STANDIN_CORRUPT");
+    int r = -1;
+    long k = -1;
+    if (e && std::sscanf(e, "%d:%ld", &r, &k) != 2) r = -1, k = -1;
+    return std::make_pair(r, k);
+  }();
+  return t;
+}
+
+// after a receive's copy (on stream s): count it, and overwrite it if it is the
+// fault-injection target
+bool after_recv(ncclComm* comm, void* dst, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return true;
+  const auto t = corrupt_target();
+  const long k = comm->recvs++;
+  if (t.first != comm->rank || t.second != k) return true;
+  return hipMemsetAsync(dst, 0xFF, std::min<size_t>(bytes, 8), s) == hipSuccess;
+}
+
+constexpr int kMaxRanks = 64;
+struct Stages { const uint64_t* p[kMaxRanks]; };   // (by value: no pointer table to allocate)
+__global__ void k_sum_u64(uint64_t* dst, Stages src, int n, size_t count) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t t = 0;
+    for (int r = 0; r < n; ++r) t += src.p[r][i];
+    dst[i] = t;
+  }
+}
 
 bool barrier(World* w) {
   std::unique_lock<std::mutex> lk(w->mu);
@@ -203,15 +265,13 @@ ncclResult_t run_collectives(ncclComm* comm, std::vector<Op>& coll) {
 ncclResult_t run_p2p(ncclComm* comm, const std::vector<Op>& p2p) {
   World* w = comm->w;
   const int me = comm->rank;
-  std::vector<char> done;
-  for (const Op& o : p2p)
-    if (o.kind == OP_SEND) done.push_back(0);
+  std::deque<SendRec> recs;   // (stable addresses)
   {
     std::lock_guard<std::mutex> lk(w->mu);
-    size_t k = 0;
     for (const Op& o : p2p)
       if (o.kind == OP_SEND) {
-        w->box[{me, o.peer}].push_back(Mail{o.src, o.count * o.esize, &done[k++]});
+        recs.emplace_back();
+        w->box[{me, o.peer}].push_back(Mail{o.src, o.count * o.esize, &recs.back(), nullptr});
       }
   }
   w->cv.notify_all();
@@ -227,19 +287,20 @@ ncclResult_t run_p2p(ncclComm* comm, const std::vector<Op>& p2p) {
       q.pop_front();
     }
     bool ok = m.bytes == o.count * o.esize;
-    if (ok && m.bytes) ok = copy(o.dst, m.src, m.bytes, o.stream);
+    if (ok && m.bytes) ok = copy(o.dst, m.src, m.bytes, o.stream) && after_recv(comm, o.dst, m.bytes, o.stream) &&
+                            hipStreamSynchronize(o.stream) == hipSuccess;
     if (!ok) rc = m.bytes == o.count * o.esize ? ncclSystemError : ncclInvalidUsage;
     {
       std::lock_guard<std::mutex> lk(w->mu);
-      *m.done = 1;
+      m.rec->done = 1;
     }
     w->cv.notify_all();
   }
   {
     std::unique_lock<std::mutex> lk(w->mu);
     if (!wait_for(w, lk, [&] {
-          for (char d : done)
-            if (!d) return false;
+          for (const SendRec& r : recs)
+            if (!r.done) return false;
           return true;
         }))
       return ncclSystemError;
@@ -247,13 +308,188 @@ ncclResult_t run_p2p(ncclComm* comm, const std::vector<Op>& p2p) {
   return rc;
 }
 
+// ---------------------------------------------------------------------------
+// async mode: the same rendezvous of the host threads, but every copy is
+// enqueued on the rank's side stream behind the events of the streams whose
+// data it moves, and the caller's stream waits for the copies' events
+
+hipEvent_t new_event() {
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
+
+ncclResult_t run_collectives_async(ncclComm* comm, std::vector<Op>& coll, hipEvent_t ready, hipStream_t caller) {
+  World* w = comm->w;
+  const int me = comm->rank;
+  const int n = w->n;
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->posted[(size_t)me] = &coll;
+    w->ev[(size_t)me] = ready;
+  }
+  if (!barrier(w)) return ncclSystemError;
+  ncclResult_t rc = ncclSuccess;
+  for (int r = 0; r < n; ++r) {
+    const std::vector<Op>& x = *w->posted[(size_t)r];
+    if (x.size() != coll.size()) rc = ncclInvalidUsage;
+    for (size_t k = 0; k < x.size() && k < coll.size(); ++k)
+      if (x[k].kind != coll[k].kind || x[k].count != coll[k].count || x[k].esize != coll[k].esize)
+        rc = ncclInvalidUsage;
+  }
+  std::vector<hipEvent_t> ready_all(w->ev);   // every rank's inputs are complete behind these
+  if (!barrier(w)) return ncclSystemError;    // (w->ev is reused below)
+  for (int r = 0; r < n && rc == ncclSuccess; ++r)
+    if (hipStreamWaitEvent(comm->side, ready_all[(size_t)r], 0) != hipSuccess) rc = ncclSystemError;
+  for (size_t ci = 0; ci < coll.size(); ++ci) {
+    const Op& o = coll[ci];
+    const size_t bytes = o.count * o.esize;
+    if (o.kind == OP_ALLGATHER) {
+      for (int r = 0; r < n && rc == ncclSuccess; ++r) {
+        const Op& x = (*w->posted[(size_t)r])[ci];
+        if (bytes && hipMemcpyAsync(static_cast<uint8_t*>(o.dst) + (size_t)r * bytes, x.src, bytes, hipMemcpyDefault,
+                                    comm->side) != hipSuccess)
+          rc = ncclSystemError;
+      }
+      continue;
+    }
+    // all-reduce (in place allowed): stage every rank's input, then sum the stages
+    hipEvent_t staged = new_event();
+    if (rc == ncclSuccess && comm->stage_bytes < bytes) {
+      if (comm->stage) (void)hipFree(comm->stage);
+      comm->stage = nullptr;
+      comm->stage_bytes = 0;
+      if (hipMalloc(&comm->stage, bytes) != hipSuccess) rc = ncclSystemError;
+      else comm->stage_bytes = bytes;
+    }
+    if (rc == ncclSuccess && bytes &&
+        hipMemcpyAsync(comm->stage, o.src, bytes, hipMemcpyDefault, comm->side) != hipSuccess)
+      rc = ncclSystemError;
+    if (!staged || hipEventRecord(staged, comm->side) != hipSuccess) rc = ncclSystemError;
+    {
+      std::lock_guard<std::mutex> lk(w->mu);
+      w->ev[(size_t)me] = staged;
+      w->stage[(size_t)me] = comm->stage;
+    }
+    if (!barrier(w)) return ncclSystemError;
+    Stages src{};
+    for (int r = 0; r < n; ++r) {
+      src.p[r] = static_cast<const uint64_t*>(w->stage[(size_t)r]);
+      if (rc == ncclSuccess && hipStreamWaitEvent(comm->side, w->ev[(size_t)r], 0) != hipSuccess) rc = ncclSystemError;
+    }
+    if (rc == ncclSuccess && o.count)
+      hipLaunchKernelGGL(k_sum_u64, dim3(std::max<size_t>(1, std::min<size_t>((o.count + 255) / 256, 1024))), dim3(256),
+                         0, comm->side, static_cast<uint64_t*>(o.dst), src, n, o.count);
+    if (!barrier(w)) return ncclSystemError;   // every rank enqueued its waits on the staged events
+    (void)hipEventDestroy(staged);
+  }
+  // the caller's stream waits for every rank's copies (they read this rank's
+  // inputs and wrote its outputs)
+  hipEvent_t done = new_event();
+  if (!done || hipEventRecord(done, comm->side) != hipSuccess) rc = ncclSystemError;
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->ev[(size_t)me] = done;
+  }
+  if (!barrier(w)) return ncclSystemError;
+  for (int r = 0; r < n; ++r)
+    if (hipStreamWaitEvent(caller, w->ev[(size_t)r], 0) != hipSuccess) rc = ncclSystemError;
+  if (!barrier(w)) return ncclSystemError;   // every rank enqueued its waits
+  (void)hipEventDestroy(done);
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    w->posted[(size_t)me] = nullptr;
+  }
+  return rc;
+}
+
+ncclResult_t run_p2p_async(ncclComm* comm, const std::vector<Op>& p2p, hipEvent_t ready, hipStream_t caller) {
+  World* w = comm->w;
+  const int me = comm->rank;
+  std::deque<SendRec> recs;
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    for (const Op& o : p2p)
+      if (o.kind == OP_SEND) {
+        recs.emplace_back();
+        w->box[{me, o.peer}].push_back(Mail{o.src, o.count * o.esize, &recs.back(), ready});
+      }
+  }
+  w->cv.notify_all();
+  ncclResult_t rc = ncclSuccess;
+  // this rank's receive buffers are free once its own stream reached the call
+  if (hipStreamWaitEvent(comm->side, ready, 0) != hipSuccess) rc = ncclSystemError;
+  for (const Op& o : p2p) {
+    if (o.kind != OP_RECV) continue;
+    Mail m{};
+    {
+      std::unique_lock<std::mutex> lk(w->mu);
+      auto& q = w->box[{o.peer, me}];
+      if (!wait_for(w, lk, [&] { return !q.empty(); })) return ncclSystemError;
+      m = q.front();
+      q.pop_front();
+    }
+    bool ok = m.bytes == o.count * o.esize;
+    hipEvent_t copied = new_event();
+    if (ok && m.bytes) {
+      ok = hipStreamWaitEvent(comm->side, m.ready, 0) == hipSuccess &&
+           hipMemcpyAsync(o.dst, m.src, m.bytes, hipMemcpyDefault, comm->side) == hipSuccess &&
+           after_recv(comm, o.dst, m.bytes, comm->side);
+    }
+    if (!copied || hipEventRecord(copied, comm->side) != hipSuccess) ok = false;
+    if (!ok) rc = m.bytes == o.count * o.esize ? ncclSystemError : ncclInvalidUsage;
+    {
+      std::lock_guard<std::mutex> lk(w->mu);
+      m.rec->copied = copied;
+      m.rec->done = 1;
+    }
+    w->cv.notify_all();
+  }
+  {
+    std::unique_lock<std::mutex> lk(w->mu);
+    if (!wait_for(w, lk, [&] {
+          for (const SendRec& r : recs)
+            if (!r.done) return false;
+          return true;
+        }))
+      return ncclSystemError;
+  }
+  // the caller's stream waits for its receives and for the copies out of its send buffers
+  hipEvent_t recv_done = new_event();
+  if (!recv_done || hipEventRecord(recv_done, comm->side) != hipSuccess ||
+      hipStreamWaitEvent(caller, recv_done, 0) != hipSuccess)
+    rc = ncclSystemError;
+  for (SendRec& r : recs)
+    if (r.copied && hipStreamWaitEvent(caller, r.copied, 0) != hipSuccess) rc = ncclSystemError;
+  for (SendRec& r : recs)
+    if (r.copied) (void)hipEventDestroy(r.copied);
+  if (recv_done) (void)hipEventDestroy(recv_done);
+  return rc;
+}
+
 // run this thread's recorded ops (one call, or one outermost group)
 ncclResult_t run_group(ncclComm* comm) {
   std::vector<Op> ops;
   ops.swap(t_rank.ops);
-  if (!sync_streams(ops)) return ncclSystemError;
   std::vector<Op> coll, p2p;
   for (const Op& o : ops) (o.kind == OP_SEND || o.kind == OP_RECV ? p2p : coll).push_back(o);
+  if (async_mode()) {   // (the engine enqueues every op of a group on its one stream)
+    const hipStream_t caller = ops.empty() ? nullptr : ops[0].stream;
+    for (const Op& o : ops)
+      if (o.stream != caller) return ncclInvalidUsage;
+    hipEvent_t ready = new_event();
+    if (!ready || hipEventRecord(ready, caller) != hipSuccess) return ncclSystemError;
+    ncclResult_t rc = ncclSuccess;
+    if (!coll.empty()) rc = run_collectives_async(comm, coll, ready, caller);
+    if (!p2p.empty()) {
+      const ncclResult_t r2 = run_p2p_async(comm, p2p, ready, caller);
+      if (rc == ncclSuccess) rc = r2;
+    }
+    // (every peer enqueued its waits on `ready` before the rendezvous above returned)
+    (void)hipEventDestroy(ready);
+    return rc;
+  }
+  if (!sync_streams(ops)) return ncclSystemError;
   ncclResult_t rc = ncclSuccess;
   if (!coll.empty()) rc = run_collectives(comm, coll);
   if (!p2p.empty()) {
@@ -299,7 +535,7 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId* id) {
 }
 
 ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank) {
-  if (!comm || nranks < 1 || rank < 0 || rank >= nranks) return ncclInvalidArgument;
+  if (!comm || nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks) return ncclInvalidArgument;
   const std::string key(commId.internal, strnlen(commId.internal, sizeof(commId.internal)));
   World* w;
   {
@@ -309,6 +545,8 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
       w = new World();
       w->n = nranks;
       w->posted.assign((size_t)nranks, nullptr);
+      w->ev.assign((size_t)nranks, nullptr);
+      w->stage.assign((size_t)nranks, nullptr);
       g_worlds[key] = w;
     } else {
       w = it->second;
@@ -320,7 +558,12 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
     ++w->joined;
   }
   if (!barrier(w)) return ncclSystemError;   // like RCCL: returns once every rank joined
-  *comm = new ncclComm{w, rank};
+  ncclComm* c = new ncclComm{w, rank};
+  if (async_mode() && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return ncclSystemError;
+  }
+  *comm = c;
   return ncclSuccess;
 }
 
@@ -341,6 +584,11 @@ ncclResult_t ncclCommDestroy(ncclComm_t comm) {
       }
     delete w;
   }
+  if (comm->side) {
+    (void)hipStreamSynchronize(comm->side);
+    (void)hipStreamDestroy(comm->side);
+  }
+  if (comm->stage) (void)hipFree(comm->stage);
   delete comm;
   return ncclSuccess;
 }

@@ -13,6 +13,13 @@ coverage and forwards (the reference sends gossip only over real links,
 Peer.py:402-404; liveness Peer.py:298-313, Seed.py:358-406).
 
 Prints "cases ok: N" and exits 0 when every case matches; raises otherwise.
+The stand-in runs synchronously or, with GP_STANDIN_ASYNC=1, only enqueues
+(copies on a side stream ordered by events, as RCCL orders its kernels), so a
+missing stream dependency in the engine shows up as a mismatch.
+
+--corrupt: one P = 2 case with GP_STANDIN_CORRUPT set by the caller (the
+stand-in overwrites one received boundary entry); every rank must fail the
+same round with GP_ERCCL and no rank may hang.  Prints "corrupt ok: ...".
 """
 import os
 import sys
@@ -34,8 +41,10 @@ STAT_KEYS = ("injected", "lost", "new_bits", "receivers", "sends", "active", "cr
 MODES = {"pull": (0.0, 0, 0), "adaptive": (10.0, 90, 16)}
 
 
-def run_ranks(pkg, g, origin, inject, P, crashes, cfg):
-    """P threads, rank k driving the context that owns partition k."""
+def run_ranks(pkg, g, origin, inject, P, crashes, cfg, errors=None):
+    """P threads, rank k driving the context that owns partition k.  Rank
+    failures raise, or with `errors` (a list) are appended to it as (rank,
+    exception) and the ranks' outputs are None."""
     uid = pkg.GossipEngine.comm_unique_id()
     engs = []
     for k in range(P):
@@ -71,7 +80,7 @@ def run_ranks(pkg, g, origin, inject, P, crashes, cfg):
             out[k] = dict(stats=stats, reports=reports, first=e.first(), digest=e.digest(), seen=e.seen(),
                           cov=e.coverage(), fwd=e.forwards(), part=e.partition())
         except BaseException as exc:   # surfaced below, after every thread ended
-            errs.append((k, repr(exc)))
+            errs.append((k, exc))
 
     ts = [threading.Thread(target=rank, args=(k,)) for k in range(P)]
     for t in ts:
@@ -80,8 +89,10 @@ def run_ranks(pkg, g, origin, inject, P, crashes, cfg):
         t.join()
     for e in engs:
         e.close()
-    if errs:
-        raise RuntimeError(f"rank failures: {errs}")
+    if errors is not None:
+        errors.extend(errs)
+    elif errs:
+        raise RuntimeError(f"rank failures: {[(k, repr(e)) for k, e in errs]}")
     return out
 
 
@@ -106,11 +117,32 @@ def check(pkg, g, origin, inject, P, crashes, cfg, ref, by_arcs, tag):
     return sum(s["xchg_rows"] for s in out[0]["stats"])
 
 
+def corrupt(pkg):
+    """Every rank fails the round whose received entries the stand-in
+    corrupted, with the same status, and the same round."""
+    assert os.environ.get("GP_STANDIN_CORRUPT"), "set GP_STANDIN_CORRUPT=rank:k"
+    g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
+    origin = pkg.overlay.random_origins(g.n, 200, seed=8)
+    errs = []
+    run_ranks(pkg, g, origin, None, 2, [], dict(track_first=1), errors=errs)
+    assert len(errs) == 2, f"expected both ranks to fail, got {[(k, repr(e)) for k, e in errs]}"
+    status = {k: getattr(e, "status", None) for k, e in errs}
+    msgs = {k: str(e) for k, e in errs}
+    assert set(status.values()) == {pkg._lib.GP_ERCCL}, msgs
+    rounds = {k: m.split("(round ")[-1] for k, m in msgs.items()}
+    assert len(set(rounds.values())) == 1, msgs
+    print(f"corrupt ok: ranks=2 status={status[0]} {msgs[0]}", flush=True)
+
+
 def main():
     pkg = _gossip_pkg.load()
     lib_path = pkg._lib.load()._name
     assert "rccl_standin" in os.path.basename(lib_path), lib_path
-    print(f"library: {lib_path}", flush=True)
+    print(f"library: {lib_path} (stand-in mode: {'async' if os.environ.get('GP_STANDIN_ASYNC') == '1' else 'sync'})",
+          flush=True)
+    if "--corrupt" in sys.argv:
+        corrupt(pkg)
+        return
     cases = 0
     # small BA overlay: every P, slice rule, churn setting and mode
     g = pkg.overlay.barabasi_albert(3001, 2, seed=8)

@@ -47,14 +47,38 @@ def test_standin_library_defines_the_rccl_calls(pkg):
     assert lib.gp_abi_version() == pkg._lib.ABI_VERSION
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(900)
-def test_exchange_rccl_multi_rank(pkg):
+def _driver(pkg, mode, *args, extra_env=None, timeout=840):
     path = _standin_lib(pkg)
     assert os.path.exists(path)
-    env = dict(os.environ, GOSSIP_HIP_LIB=path)
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "rccl_standin_driver.py")], env=env,
-                       capture_output=True, text=True, timeout=840)
+    env = dict(os.environ, GOSSIP_HIP_LIB=path, GP_STANDIN_ASYNC="1" if mode == "async" else "0")
+    env.pop("GP_STANDIN_CORRUPT", None)
+    env.update(extra_env or {})
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "rccl_standin_driver.py"), *args], env=env,
+                       capture_output=True, text=True, timeout=timeout)
     print(r.stdout[-6000:])
     assert r.returncode == 0, r.stderr[-6000:]
-    assert "cases ok: 27" in r.stdout
+    return r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_exchange_rccl_multi_rank(pkg, mode):
+    """27 partitioned runs through exchange_rccl against the oracle, with the
+    stand-in synchronous or enqueue-only (async: RCCL's stream semantics, so a
+    missing stream dependency in the engine would show up as a mismatch)."""
+    out = _driver(pkg, mode)
+    assert f"stand-in mode: {mode}" in out
+    assert "cases ok: 27" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_exchange_rccl_corrupt_entry_fails_every_rank(pkg, mode):
+    """A boundary entry corrupted in flight (the stand-in overwrites rank 1's
+    third non-empty receive) fails the round on both ranks with GP_ERCCL: the
+    unpack checks every entry against the exchange plan before writing, and
+    the counters' all-reduce carries the count to every rank."""
+    out = _driver(pkg, mode, "--corrupt", extra_env={"GP_STANDIN_CORRUPT": "1:2"}, timeout=280)
+    assert "corrupt ok: ranks=2 status=-5" in out
