@@ -20,29 +20,49 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
-SET = ("k_mklm", "k_expand", "k_hub_partial", "k_hub_final")
+SET = ("k_mklm", "k_expand", "k_hub_partial", "k_hub_final", "k_acc_clear",
+       "k_active_list", "k_push", "k_touch_list", "k_apply")
+
+
+def _kind(name):
+    for key, kind in (("k_mklm", "mklm"), ("k_expand", "pull"), ("k_hub_", "hub"), ("k_acc_clear", "clear"),
+                      ("k_active_list", "push"), ("k_push", "push"), ("k_touch_list", "apply"), ("k_apply", "apply")):
+        if key in name:
+            return kind
+    return None
 
 
 def load(d, counter):
-    """Counter per pull launch: a k_expand* dispatch opens a launch unless the
-    line-mask pass k_mklm just opened it (it runs first, inside the pull's
-    events); the hub dispatches after it (before the next pull) add to it."""
+    """Counter per pull launch -- the kernels kernel_ms brackets: a k_expand*
+    dispatch opens a launch unless the line-mask pass k_mklm just opened it (it
+    runs first, inside the pull's events); the hub dispatches and a
+    degree-split round's k_acc_clear after it add to it, and so does the push
+    half before it (k_active_list / k_push / k_push_big directly followed by
+    the pull; push rounds are followed by k_touch_list / k_apply instead and
+    are not counted)."""
     path = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     per, kind = {}, {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in SET):
+        kd = _kind(r["Kernel_Name"])
+        if r["Counter_Name"] != counter or kd is None:
             continue
         k = int(r["Dispatch_Id"])
         per[k] = per.get(k, 0.0) + float(r["Counter_Value"])
-        kind[k] = "mklm" if "k_mklm" in r["Kernel_Name"] else ("pull" if "k_expand" in r["Kernel_Name"] else "hub")
+        kind[k] = kd
     out = []
-    prev = None
+    prev, pending = None, 0.0
     for k in sorted(per):
-        if kind[k] == "mklm" or (kind[k] == "pull" and prev != "mklm"):
-            out.append(per[k])
+        kd = kind[k]
+        if kd == "push":
+            pending += per[k]
+        elif kd == "apply":
+            pending = 0.0
+        elif kd == "mklm" or (kd == "pull" and prev != "mklm"):
+            out.append(per[k] + pending)
+            pending = 0.0
         elif out:
             out[-1] += per[k]
-        prev = kind[k]
+        prev = kd
     return out
 
 
@@ -72,7 +92,8 @@ def main():
     th = sum(x["fetch_GB"] + x["write_GB"] for x in rows)
     tm = sum(x["kernel_ms"] for x in rows)
     print(f"| all {len(rows)} launches | {ta:.2f} | | | {th:.2f} | {th / ta:.3f} | {tm:.2f} | {th / tm:.2f} |")
-    out = {"kernel": "k_mklm (line-mask rounds) + k_expand + k_hub_partial + k_hub_final", "launches": len(rows), "traffic_bytes_per_launch": th * 1e9 / len(rows),
+    out = {"kernel": "k_mklm (line-mask rounds) + k_expand + k_hub_partial + k_hub_final (+ a degree-split round's "
+                     "push half and k_acc_clear)", "launches": len(rows), "traffic_bytes_per_launch": th * 1e9 / len(rows),
            "alg_bytes_per_launch": ta * 1e9 / len(rows), "kernel_ms_per_launch": tm / len(rows),
            "rounds": rows, "config": bench["config"],
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bytes = "

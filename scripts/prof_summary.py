@@ -61,5 +61,39 @@ def main():
                   f"{(e['pull_ms'] + e['hub_ms']) / e['launches']:.3f} ms per launch")
 
 
+    # per dispatch, from the kernel trace beside the stats: the pull launch as
+    # kernel_ms brackets it (a degree-split round's push half before the pull
+    # kernel and its k_acc_clear after the hub passes included; push rounds --
+    # k_push followed by k_touch_list / k_apply -- excluded)
+    import glob
+    import os
+    trace = glob.glob(os.path.join(os.path.dirname(path), "*kernel_trace.csv"))
+    if trace:
+        launches, pending, prev = [], 0.0, None
+        recs = sorted(csv.DictReader(open(trace[0])), key=lambda r: int(r["Start_Timestamp"]))
+        for r in recs:
+            n = short(r["Kernel_Name"])
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            kd = ("mklm" if "k_mklm" in n else "pull" if "k_expand" in n else "hub" if "k_hub_" in n else
+                  "clear" if "k_acc_clear" in n else "push" if ("k_active_list" in n or "k_push" in n) else
+                  "apply" if ("k_touch_list" in n or "k_apply" in n) else None)
+            if kd is None:
+                continue
+            if kd == "push":
+                pending += dur
+            elif kd == "apply":
+                pending = 0.0
+            elif kd == "mklm" or (kd == "pull" and prev != "mklm"):
+                launches.append(dur + pending)
+                pending = 0.0
+            elif launches:
+                launches[-1] += dur
+            prev = kd
+        if launches:
+            print(f"\npull launches from the kernel trace (the kernels kernel_ms brackets, incl. a degree-split "
+                  f"round's push half and clear): {len(launches)} launches, {sum(launches):.3f} ms, "
+                  f"{sum(launches) / len(launches):.3f} ms per launch")
+
+
 if __name__ == "__main__":
     main()

@@ -341,6 +341,19 @@ ncclResult_t run_collectives_async(ncclComm* comm, std::vector<Op>& coll, hipEve
   if (!barrier(w)) return ncclSystemError;    // (w->ev is reused below)
   for (int r = 0; r < n && rc == ncclSuccess; ++r)
     if (hipStreamWaitEvent(comm->side, ready_all[(size_t)r], 0) != hipSuccess) rc = ncclSystemError;
+  // every all-reduce of the group stages into its own part of the stage buffer
+  // (another rank's sum may still read this rank's stage of an earlier op)
+  size_t stage_total = 0;
+  for (const Op& o : coll)
+    if (o.kind == OP_ALLREDUCE) stage_total += o.count * o.esize;
+  if (rc == ncclSuccess && comm->stage_bytes < stage_total) {
+    if (comm->stage) (void)hipFree(comm->stage);
+    comm->stage = nullptr;
+    comm->stage_bytes = 0;
+    if (hipMalloc(&comm->stage, stage_total) != hipSuccess) rc = ncclSystemError;
+    else comm->stage_bytes = stage_total;
+  }
+  size_t stage_off = 0;
   for (size_t ci = 0; ci < coll.size(); ++ci) {
     const Op& o = coll[ci];
     const size_t bytes = o.count * o.esize;
@@ -355,15 +368,8 @@ ncclResult_t run_collectives_async(ncclComm* comm, std::vector<Op>& coll, hipEve
     }
     // all-reduce (in place allowed): stage every rank's input, then sum the stages
     hipEvent_t staged = new_event();
-    if (rc == ncclSuccess && comm->stage_bytes < bytes) {
-      if (comm->stage) (void)hipFree(comm->stage);
-      comm->stage = nullptr;
-      comm->stage_bytes = 0;
-      if (hipMalloc(&comm->stage, bytes) != hipSuccess) rc = ncclSystemError;
-      else comm->stage_bytes = bytes;
-    }
-    if (rc == ncclSuccess && bytes &&
-        hipMemcpyAsync(comm->stage, o.src, bytes, hipMemcpyDefault, comm->side) != hipSuccess)
+    uint8_t* my_stage = static_cast<uint8_t*>(comm->stage) + stage_off;
+    if (rc == ncclSuccess && bytes && hipMemcpyAsync(my_stage, o.src, bytes, hipMemcpyDefault, comm->side) != hipSuccess)
       rc = ncclSystemError;
     if (!staged || hipEventRecord(staged, comm->side) != hipSuccess) rc = ncclSystemError;
     {
@@ -373,8 +379,8 @@ ncclResult_t run_collectives_async(ncclComm* comm, std::vector<Op>& coll, hipEve
     }
     if (!barrier(w)) return ncclSystemError;
     Stages src{};
-    for (int r = 0; r < n; ++r) {
-      src.p[r] = static_cast<const uint64_t*>(w->stage[(size_t)r]);
+    for (int r = 0; r < n; ++r) {   // (the ranks' op sequences match: the same offset on every rank)
+      src.p[r] = reinterpret_cast<const uint64_t*>(static_cast<const uint8_t*>(w->stage[(size_t)r]) + stage_off);
       if (rc == ncclSuccess && hipStreamWaitEvent(comm->side, w->ev[(size_t)r], 0) != hipSuccess) rc = ncclSystemError;
     }
     if (rc == ncclSuccess && o.count)
@@ -382,6 +388,7 @@ ncclResult_t run_collectives_async(ncclComm* comm, std::vector<Op>& coll, hipEve
                          0, comm->side, static_cast<uint64_t*>(o.dst), src, n, o.count);
     if (!barrier(w)) return ncclSystemError;   // every rank enqueued its waits on the staged events
     (void)hipEventDestroy(staged);
+    stage_off += bytes;
   }
   // the caller's stream waits for every rank's copies (they read this rank's
   // inputs and wrote its outputs)
