@@ -6,8 +6,8 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/emu
 one() {   # tag, args...
   local tag=$1; shift
-  timeout -k 10 120 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > gpurun_out/emu/$tag.json 2> gpurun_out/emu/$tag.err || exit 1
-  python3 -c "import json,sys; d=json.load(open('gpurun_out/emu/$tag.json')); print('%-22s %8.2f ms  rounds %.0f  sends %d' % ('$tag', d['ms_per_step'], d['config']['rounds_per_step'], d['config']['edge_deliveries_per_step']))"
+  timeout -k 10 120 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --profile-steps "$@" > gpurun_out/emu/$tag.json 2> gpurun_out/emu/$tag.err || exit 1
+  python3 scripts/emu_line.py $tag gpurun_out/emu/$tag.json gpurun_out/emu/$tag.err
 }
 one c4
 for N in ${NS:-2 4 8}; do
