@@ -85,8 +85,10 @@ __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirs
 // Per-wave counters live in LDS (one row per wave, written by lane 0 only):
 // every update is wave-uniform, and keeping NST u64 counters out of the VGPR
 // file is worth several waves per SIMD of occupancy in the gather kernels.
+// (NW: waves per block of the kernel -- the one-wave pull kernels keep one row)
+template <int NW = WAVES>
 __device__ __forceinline__ u64* stats_lds() {
-  __shared__ u64 rows[WAVES][NST];
+  __shared__ u64 rows[NW][NST];
   return &rows[0][0];
 }
 struct WaveStats {
@@ -96,24 +98,26 @@ struct WaveStats {
     if (lead) row[k] += x;
   }
 };
+template <int NW = WAVES>
 __device__ __forceinline__ void ws_zero(WaveStats& s) {
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
-  s.row = stats_lds() + wib * NST;
+  s.row = stats_lds<NW>() + wib * NST;
   s.lead = lane == 0;
   if (lane < NST) s.row[lane] = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+template <int NW = WAVES>
 __device__ inline void flush_stats(const WaveStats& s, u64* __restrict__ partial) {
   (void)s;
-  u64* red = stats_lds();
+  u64* red = stats_lds<NW>();
   __syncthreads();
   if (threadIdx.x < NST) {
     u64 t = 0;
 #pragma unroll
-    for (int w = 0; w < WAVES; ++w)
-      if (w < (int)(blockDim.x >> 6)) t += red[w * NST + threadIdx.x];   // (pull kernels: EWAVES)
+    for (int w = 0; w < NW; ++w)
+      if (w < (int)(blockDim.x >> 6)) t += red[w * NST + threadIdx.x];
     if (t) atomicAdd(&partial[(size_t)threadIdx.x * NPART + (blockIdx.x % NPART)], t);
   }
 }

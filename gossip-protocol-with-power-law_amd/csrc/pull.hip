@@ -212,7 +212,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
   constexpr bool ALIVE = (MODE & SCAN_ALIVE) != 0;
   constexpr int SCAN = MODE & ~SCAN_ALIVE;
   WaveStats st;
-  ws_zero(st);
+  ws_zero<EWAVES>(st);
   const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * 64;
   if (base < a.nloc) {
     const int64_t li = base + lane;
@@ -461,7 +461,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
       if (sat && ((sat >> lane) & 1ull)) a.state[a.vbegin + li] |= ST_SATED;
     }
   }
-  flush_stats(st, a.partial);
+  flush_stats<EWAVES>(st, a.partial);
 }
 
 // ---------------------------------------------------------------------------
@@ -475,18 +475,22 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
 // receiver side then runs lane-parallel, one receiver per lane.  No early exit
 // (narrow rows are cheap next to the arc scan).
 constexpr int FLAT_CAP = 512;   // arc positions per owner window
-// row wave-instructions in flight per lane (VGPRs vs occupancy: 2 -> 66 VGPRs
-// at W = 8).  Measured on the message shards (same box A/B): W = 8 (64-B rows,
-// 16 per instruction) 15.6 -> 15.2 ms with 3 for a 512-message shard; W = 16
-// 28.3 -> 24.4 ms with 4 and 22.9 ms with 6 for a 1024-message shard (8: 25.6)
+// row wave-instructions in flight per lane (VGPRs vs occupancy).  Measured on
+// the message shards (same box A/B): W = 8 (64-B rows, 16 per instruction)
+// 15.6 -> 15.2 ms with 3 against 2 for a 512-message shard (round 3 of the
+// build), and 5 against 3 at HEAD of round 5 (72 against 76 VGPRs; 4 takes 90):
+// ranks 7 / 0 of the N = 8 job 12.12 -> 11.83 / 10.47 -> 10.16 ms
+// (profiles/r05_ab_flat_w8.txt; forcing 8 waves per SIMD at 64 VGPRs was
+// slower, 12.0-12.2 ms); W = 16 28.3 -> 24.4 ms with 4 and 22.9 ms with 6 for
+// a 1024-message shard (8: 25.6).  W < 8: 3 (5 costs W = 1 16 VGPRs)
 #ifndef GP_FLAT_RIF_NARROW
-#define GP_FLAT_RIF_NARROW 3
+#define GP_FLAT_RIF_NARROW 5
 #endif
 #ifndef GP_FLAT_RIF_WIDE
 #define GP_FLAT_RIF_WIDE 6
 #endif
 template <int W>
-struct FlatRIF { static constexpr int value = W >= 16 ? GP_FLAT_RIF_WIDE : GP_FLAT_RIF_NARROW; };
+struct FlatRIF { static constexpr int value = W >= 16 ? GP_FLAT_RIF_WIDE : W == 8 ? GP_FLAT_RIF_NARROW : 3; };
 // receivers per wave: 64, or 32 at W = 32 so that the LDS accumulators (8 KB
 // per wave) leave room for 4 blocks per CU
 template <int W>
@@ -495,14 +499,22 @@ template <int W>
 struct FlatLds {
   static constexpr int NR = FlatNR<W>::value;
   u64 acc[NR][W];               // OR accumulators of the wave's NR receivers
-  int32_t idx[64];              // active neighbours of one chunk
-  int8_t vtx[64];               // their receiver (lane) in the wave
-  int8_t own[FLAT_CAP];         // receiver lane owning each arc position of the window
-  uint32_t tot[NR];             // receiver side: new bits of receiver k
-  u64 dig[NR];                  // its digest terms
-  int8_t rd[NR];                // its seen row was read
-  u64 alive[W];                 // OR of the new rows this wave wrote (alive_next); W words, so
-                                // that W = 16 keeps 4 blocks per CU
+  // the passes' staging and the receiver side's words share their bytes (the
+  // receiver side starts after the last pass): W = 8 takes 4,928 B + 176 B
+  // of counters, so LDS no longer caps its waves (VGPRs do: 7 per SIMD)
+  union {
+    struct {
+      int32_t idx[64];          // active neighbours of one chunk
+      int8_t vtx[64];           // their receiver (lane) in the wave
+      int8_t own[FLAT_CAP];     // receiver lane owning each arc position of the window
+    };
+    struct {
+      uint16_t tot[NR];         // receiver side: new bits of receiver k (<= 64 W)
+      u64 dig[NR];              // its digest terms
+      int8_t rd[NR];            // between passes: still missing messages; receiver side: its seen row was read
+      u64 alive[W];             // receiver side: OR of the new rows this wave wrote (alive_next)
+    };
+  };
 };
 
 // one flat pass: the arcs [start, start + sdeg) of every lane's receiver, as
@@ -650,10 +662,9 @@ __global__ __launch_bounds__(EBLOCK) void k_expand_flat(ExpandArgs a) {
   FlatLds<W>& F = s_f[wib];
   constexpr int NR = FlatNR<W>::value;
   WaveStats st;
-  ws_zero(st);
+  ws_zero<EWAVES>(st);
   const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * NR;
   if (base < a.nloc) {
-    alive_zero<W>(a, F.alive, lane);
     // per-lane state is reloaded (coalesced) where it is needed rather than
     // kept live across the passes: VGPRs are what bound this kernel's waves
     const int64_t li = base + lane;
@@ -760,6 +771,8 @@ __global__ __launch_bounds__(EBLOCK) void k_expand_flat(ExpandArgs a) {
     // writes nothing.  Per-receiver words go to F.tot / F.dig, then one
     // coalesced commit with one receiver per lane.
     wave_sync_lds();
+    alive_zero<W>(a, F.alive, lane);   // (shares its bytes with the passes' staging)
+    wave_sync_lds();
     const uint32_t slot_of = need ? a.sp[v] : SLOT_NONE;
     for (int r0 = 0; r0 < NR; r0 += RPI) {
       const int r = r0 + g;
@@ -824,7 +837,7 @@ __global__ __launch_bounds__(EBLOCK) void k_expand_flat(ExpandArgs a) {
     alive_flush<W>(a, F.alive, lane);
     }   // needm
   }
-  flush_stats(st, a.partial);
+  flush_stats<EWAVES>(st, a.partial);
 }
 
 // ---------------------------------------------------------------------------
