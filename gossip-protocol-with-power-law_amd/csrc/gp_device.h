@@ -877,7 +877,7 @@ template <int W> void launch_push_w(Ctx* c, ExpandArgs a);            // a push 
 template <int W> void launch_split_push_w(Ctx* c, const ExpandArgs& a);   // degree-split round: the push half
 template <int W> void launch_acc_clear_w(Ctx* c);                     // ... and its accumulator back to zero
 // hub.hip: the hub receivers of a pull round (partials, then the final rows)
-template <int W> void launch_hubs_w(Ctx* c, const ExpandArgs& a, bool unfiltered);
+template <int W> void launch_hubs_w(Ctx* c, const ExpandArgs& a, bool unfiltered, bool lines);
 // liveness.hip: L_r (crash draws, miss counters, detection, seed removal)
 int launch_liveness(Ctx* c);
 constexpr int DET_CAP = 16384;   // deferred (big) detection candidates per round (more: walked in-wave)

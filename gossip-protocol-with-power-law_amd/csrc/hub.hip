@@ -70,24 +70,35 @@ __global__ __launch_bounds__(HBLOCK) void k_hub_final(ExpandArgs a) {
 }
 
 
+// (lines: the round's pull read its senders' line masks, SCAN_LINES -- the hub
+// chunks probe the same masks and gather only the named 128-B lines: round 2
+// C4 12.85 -> 12.70 ms, C5 42.35 -> 40.99 ms, profiles/r05_ab_hub_lines.txt)
 template <int W>
-void launch_hubs_w(Ctx* c, const ExpandArgs& a, bool unfiltered) {
+void launch_hubs_w(Ctx* c, const ExpandArgs& a, bool unfiltered, bool lines) {
   ExpandArgs h = a;
   h.n_items = c->n_hub_items;
   const dim3 grid(grid_for(h.n_items, HWAVES));
-  if (unfiltered)
+  bool done = false;
+  if constexpr (W == 64) {
+    if (lines && !unfiltered) {
+      hipLaunchKernelGGL((k_hub_partial<W, SCAN_FILTERED | SCAN_LINES>), grid, dim3(HBLOCK), 0, c->stream, h);
+      done = true;
+    }
+  }
+  if (done) {
+  } else if (unfiltered)
     hipLaunchKernelGGL((k_hub_partial<W, SCAN_UNFILTERED>), grid, dim3(HBLOCK), 0, c->stream, h);
   else
     hipLaunchKernelGGL((k_hub_partial<W, SCAN_FILTERED>), grid, dim3(HBLOCK), 0, c->stream, h);
   h.n_items = c->n_hubs;
   hipLaunchKernelGGL(k_hub_final<W>, dim3(grid_for(h.n_items, HWAVES)), dim3(HBLOCK), 0, c->stream, h);
 }
-template void launch_hubs_w<1>(Ctx*, const ExpandArgs&, bool);
-template void launch_hubs_w<2>(Ctx*, const ExpandArgs&, bool);
-template void launch_hubs_w<4>(Ctx*, const ExpandArgs&, bool);
-template void launch_hubs_w<8>(Ctx*, const ExpandArgs&, bool);
-template void launch_hubs_w<16>(Ctx*, const ExpandArgs&, bool);
-template void launch_hubs_w<32>(Ctx*, const ExpandArgs&, bool);
-template void launch_hubs_w<64>(Ctx*, const ExpandArgs&, bool);
+template void launch_hubs_w<1>(Ctx*, const ExpandArgs&, bool, bool);
+template void launch_hubs_w<2>(Ctx*, const ExpandArgs&, bool, bool);
+template void launch_hubs_w<4>(Ctx*, const ExpandArgs&, bool, bool);
+template void launch_hubs_w<8>(Ctx*, const ExpandArgs&, bool, bool);
+template void launch_hubs_w<16>(Ctx*, const ExpandArgs&, bool, bool);
+template void launch_hubs_w<32>(Ctx*, const ExpandArgs&, bool, bool);
+template void launch_hubs_w<64>(Ctx*, const ExpandArgs&, bool, bool);
 
 }  // namespace gp

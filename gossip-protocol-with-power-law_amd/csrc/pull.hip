@@ -1297,7 +1297,7 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
         hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED>), grid, dim3(EBLOCK), 0, c->stream, a);
     }
   }
-  if (c->n_hub_items > 0) launch_hubs_w<W>(c, a, mode == SCAN_UNFILTERED);
+  if (c->n_hub_items > 0) launch_hubs_w<W>(c, a, mode == SCAN_UNFILTERED, c->lines_ran);
   // kernel_ms brackets the pull kernel and the hub passes: the round's
   // counters (row bytes, arcs scanned, rows written) include the hubs' share
   if (a.prehi) launch_acc_clear_w<W>(c);   // degree-split round: the accumulator back to all-zero
