@@ -25,7 +25,10 @@ __global__ __launch_bounds__(HBLOCK) void k_hub_partial(ExpandArgs a) {
       const bool ee = a.early_exit != 0;
       u64x2 want = {0, 0};
       if (ee) want = early_exit_target<W>(a, h.v, s_w[wib], g, lw, a.sp[h.v], a.midx[h.v]);
-      gather_scan<W, MODE>(a, h.beg, h.end, s_w[wib], lane, g, lw, acc, st, ee, want);
+      // degree-split rounds: the chunk's share of the gather-order prefix of
+      // big senders (the push half ORed the others into the accumulator row)
+      const int64_t hend = a.prehi ? min(h.end, a.row_ptr[h.v] + (int64_t)a.prehi[h.v]) : h.end;
+      if (hend > h.beg) gather_scan<W, MODE>(a, h.beg, hend, s_w[wib], lane, g, lw, acc, st, ee, want);
       reduce_slots<W>(acc);
     }
     const bool nz = __any((acc.x | acc.y) != 0);
