@@ -344,6 +344,9 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.hub_item_ptr = c->d_hub_item_ptr;
   a.hub_partial = c->d_hub_partial;
   a.hub_pnz = c->d_hub_pnz;
+  a.hub_done = c->d_hub_done;
+  if (++c->hub_epoch == 0) c->hub_epoch = 1;   // (wraps after 2^32 launches: 0 is the never-set value)
+  a.hub_epoch = c->hub_epoch;
   a.vbegin = 0;   // kernels address local ids: owned vertices are [0, nloc)
   a.nloc = c->nloc();
   a.m_total = c->m;

@@ -188,6 +188,8 @@ struct ExpandArgs {
   const int32_t* __restrict__ hub_item_ptr;
   u64* __restrict__ hub_partial;
   uint32_t* __restrict__ hub_pnz;
+  uint32_t* __restrict__ hub_done;     // [n_hubs] early-exit rounds: = hub_epoch once a chunk covered its hub's target
+  uint32_t hub_epoch;                  // this pull launch's stamp (never 0, never repeats within a context)
   // push mode
   const int64_t* __restrict__ orp;     // out-CSR (undirected: == row_ptr/col)
   const int32_t* __restrict__ ocol;

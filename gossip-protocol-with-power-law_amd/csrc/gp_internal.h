@@ -199,6 +199,8 @@ struct Ctx {
     return it == inject.end() ? 0 : it->second.cnt;
   }
   int32_t* d_gcol = nullptr;        // [nnz] in-CSR columns, rows sorted by neighbour degree desc
+  uint32_t* d_hub_done = nullptr;   // [n_hubs] early-exit rounds: a chunk covered its hub's target (hub.hip)
+  uint32_t hub_epoch = 0;           // stamp of the last pull launch (k_hub_partial's hub_done)
   int32_t* d_prehi = nullptr;       // [n] degree-split rounds: gather-order prefix of senders with
                                     //   in-degree >= prehi_deg (build_prehi, built on first use)
   int32_t prehi_deg = 0;

@@ -28,7 +28,30 @@ __global__ __launch_bounds__(HBLOCK) void k_hub_partial(ExpandArgs a) {
       // degree-split rounds: the chunk's share of the gather-order prefix of
       // big senders (the push half ORed the others into the accumulator row)
       const int64_t hend = a.prehi ? min(h.end, a.row_ptr[h.v] + (int64_t)a.prehi[h.v]) : h.end;
-      if (hend > h.beg) gather_scan<W, MODE>(a, h.beg, hend, s_w[wib], lane, g, lw, acc, st, ee, want);
+      // early-exit rounds: a chunk that covers the hub's whole target says so
+      // (hub_done = this launch's stamp), and the hub's other chunks stop at
+      // their next 512 arcs -- the OR of all chunks is then exactly the target
+      // whatever they gathered (every row is a subset of the component's
+      // messages; under liveness nothing outside F_r is new, ExpandArgs)
+      constexpr int64_t SUB = 512;
+      for (int64_t s0 = h.beg; s0 < hend; s0 += SUB) {
+        if (ee && a.hub_done) {
+          uint32_t f = 0;
+          if (lane == 0) f = __hip_atomic_load(a.hub_done + h.hub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)__builtin_amdgcn_readfirstlane((int)f) == a.hub_epoch) break;
+        }
+        gather_scan<W, MODE>(a, s0, min(hend, s0 + SUB), s_w[wib], lane, g, lw, acc, st, ee, want);
+        if (ee) {
+          u64x2 t = acc;
+          reduce_slots<W>(t);
+          const u64x2 miss = want & ~t;
+          if (!__any((miss.x | miss.y) != 0ull)) {
+            if (lane == 0 && a.hub_done)
+              __hip_atomic_store(a.hub_done + h.hub, a.hub_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
       reduce_slots<W>(acc);
     }
     const bool nz = __any((acc.x | acc.y) != 0);

@@ -152,6 +152,9 @@ int build_hubs(Ctx* c) {
   GP_TRY(dalloc(&c->d_hubs, hubs.size()));
   GP_TRY(dalloc(&c->d_hub_item_ptr, ptr.size()));
   GP_TRY(dalloc(&c->d_hub_pnz, c->h_hub_items.size()));
+  GP_TRY(dalloc(&c->d_hub_done, std::max<size_t>(hubs.size(), 1)));
+  GP_HIP(hipMemsetAsync(c->d_hub_done, 0, std::max<size_t>(hubs.size(), 1) * 4, c->stream));
+  c->hub_epoch = 0;
   if (!c->h_hub_items.empty())
     GP_TRY(copy_sync(c, c->d_hub_items, c->h_hub_items.data(), c->h_hub_items.size() * sizeof(HubItem),
                      hipMemcpyHostToDevice));
@@ -523,7 +526,7 @@ void gp_destroy(gp_ctx* c) {
   dfree(&c->d_det_big); dfree(&c->d_det_pre); dfree(&c->d_det_live); dfree(&c->d_det_cur); dfree(&c->d_det_base);
   dfree(&c->d_msg_cov); dfree(&c->d_reports); dfree(&c->d_stats);
   dfree(&c->d_hub_items); dfree(&c->d_hubs); dfree(&c->d_hub_item_ptr);
-  dfree(&c->d_hub_partial); dfree(&c->d_hub_pnz);
+  dfree(&c->d_hub_partial); dfree(&c->d_hub_pnz); dfree(&c->d_hub_done);
   bitcount_free(c);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
