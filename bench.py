@@ -15,6 +15,7 @@ distributes the RCCL id and the timings: no PyTorch in this process).
 """
 import argparse
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -122,8 +123,13 @@ def round_bytes(st, words, nloc):
     # degree-split rounds (scan bit 32): the push half's accumulator updates,
     # 8 B each (kernel_ms brackets the push half and the clear too)
     split = 8 * st.get("atomics", 0) if st.get("scan", 0) & 32 else 0
+    # done-probe rounds (scan bit 64): an 8-B done-bitmap word per scanned arc;
+    # receivers committed as aliases of their component row write no row,
+    # only their per-vertex words
+    if st.get("scan", 0) & 64:
+        arcs += 8 * st["arcs_scanned"]
     return (30 * nloc + arcs + st["row_bytes"] + w8 * st["seen_rows_read"]
-            + (w8 + 23) * st["rows_written"] + w8 * st.get("lm_rows", 0) + split)
+            + (w8 + 23) * st["rows_written"] + 23 * st.get("aliased", 0) + w8 * st.get("lm_rows", 0) + split)
 
 
 def message_table(origin, nranks, assign, order, message_shard):
@@ -214,16 +220,16 @@ def _host():
 
 
 def cpu_baseline(args, eng, origin, pkg):
-    """Two CPU legs, timed on this box's host cores (reported beside the GPU
+    """CPU legs, timed on this box's host cores (reported beside the GPU
     line, never the target):
-      port     oracle/gossip_oracle.c (OpenMP, every thread this process may
-               use: OMP_NUM_THREADS, else the affinity set) running ALL
+      port     oracle/gossip_oracle.c (OpenMP) with every thread of the
+               process's affinity set -- `value` -- and again with the
+               OMP_NUM_THREADS share when the environment sets fewer, running ALL
                `messages` (W = 64 words per Message-List row, the GPU's layout)
                to quiescence on a 2^cpu_log2n-vertex overlay of the same
                Chung-Lu recipe and seed: by default the workload itself, on
                the overlay the GPU ran (C4 2^24 x 4096: ~30 s on 16 threads;
                C5 2^26 x 4096 with churn, the same crash stream: ~100 s);
-               this leg is `value`;
       harness  oracle/harness.py, the reference's per-peer Message-List logic
                (sha256 digests in a set per peer, Peer.py:175-216, 395-408) plus
                forwarding, single-core, on BASELINE config 2 (10^4-node BA(m=2),
@@ -242,17 +248,25 @@ def cpu_baseline(args, eng, origin, pkg):
             side.build_chung_lu(ncpu, args.dbar, args.gamma, args.seed)
             g = side.graph()
     o = pkg.overlay.random_origins(ncpu, args.messages, seed=args.seed)
-    t0 = time.perf_counter()
-    ref = oracle_lib.run(g, o, nthreads=threads, want_forwards=False, want_seen=False, churn=churn,
-                         p_fail=args.p_fail if churn else 0.0, churn_seed=args.seed)
-    dt = time.perf_counter() - t0
-    sends = sum(s["sends"] for s in ref["stats"])
-    out = {"value": sends / dt / 1e9, "unit": "GTEPS", "cores": threads, "kind": "port",
-           "sample": f"oracle/gossip_oracle.c, Chung-Lu gamma={args.gamma} d={args.dbar:g} seed {args.seed} at "
-                     f"2^{args.cpu_log2n} vertices ({g.nnz} arcs{', the GPU run overlay' if ncpu == eng.n else ''}), "
-                     f"all {len(o)} messages (W = 64), full run"
-                     f"{' with churn' if churn else ''} ({ref['rounds']} rounds, {sends} edge-deliveries, "
-                     f"{dt:.1f} s, {threads} OpenMP threads)",
+    # port legs: every thread this process may use (the box's affinity set:
+    # SURVEY.md §8d "all host cores"), and the OMP_NUM_THREADS share the
+    # environment grants (16 on the GPU box) when that is fewer
+    counts = [args.cpu_threads] if args.cpu_threads else sorted({aff, threads}, reverse=True)
+    legs = []
+    for t in counts:
+        t0 = time.perf_counter()
+        ref = oracle_lib.run(g, o, nthreads=t, want_forwards=False, want_seen=False, churn=churn,
+                             p_fail=args.p_fail if churn else 0.0, churn_seed=args.seed)
+        dt = time.perf_counter() - t0
+        sends = sum(s["sends"] for s in ref["stats"])
+        legs.append({"kind": "port", "value": sends / dt / 1e9, "unit": "GTEPS", "cores": t,
+                     "sample": f"oracle/gossip_oracle.c, Chung-Lu gamma={args.gamma} d={args.dbar:g} seed {args.seed} "
+                               f"at 2^{args.cpu_log2n} vertices ({g.nnz} arcs"
+                               f"{', the GPU run overlay' if ncpu == eng.n else ''}), all {len(o)} messages (W = 64), "
+                               f"full run{' with churn' if churn else ''} ({ref['rounds']} rounds, {sends} "
+                               f"edge-deliveries, {dt:.1f} s, {t} OpenMP threads of {nproc})"})
+    out = {"value": legs[0]["value"], "unit": "GTEPS", "cores": legs[0]["cores"], "kind": "port",
+           "sample": legs[0]["sample"],
            "host": {"nproc": nproc, "affinity": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
                     "cpu_model": model}}
     # leg 2: the per-peer Python harness, single core, BASELINE config 2
@@ -263,13 +277,38 @@ def cpu_baseline(args, eng, origin, pkg):
     hr = harness.run(h.n, in_lists, False, ho, [0] * len(ho))
     hdt = time.perf_counter() - t0
     hs = sum(s["sends"] for s in hr["stats"])
-    out["legs"] = [
-        {"kind": "port", "value": out["value"], "unit": "GTEPS", "cores": threads, "sample": out["sample"]},
+    out["legs"] = legs + [
         {"kind": "harness", "value": hs / hdt / 1e9, "unit": "GTEPS", "cores": 1,
          "sample": f"oracle/harness.py (per-peer sha256 Message-List sets), 10^4-node BA(m=2), 64 messages, "
                    f"{hr['rounds']} rounds, {hs} edge-deliveries, {hdt:.2f} s, 1 core"},
     ]
     return out
+
+
+def _fp(a):
+    """64-bit fingerprint of an output array (sha256 of its bytes)."""
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+def job_record(eng, stats, m_total, job, partitioned):
+    """The whole run's record as the line reports it, so that 1-GPU and N-GPU
+    lines compare directly: per-round receivers / active counts and
+    fingerprints of the per-vertex digest and the per-message coverage /
+    forwards (a shard job: the combined job outputs; one GPU: the context's
+    own).  None for the vertex partition (each rank holds its slice)."""
+    if partitioned:
+        return None
+    dig = eng.job_digest() if job else eng.digest()
+    cov = eng.job_coverage(m_total) if job else eng.coverage()
+    try:
+        fwd = _fp(eng.job_forwards(m_total) if job else eng.forwards())
+    except Exception as e:   # churn without track_msg_forwards: GP_ENOTRACK
+        if getattr(e, "status", None) != -6:
+            raise
+        fwd = None
+    return {"rounds": len(stats), "receivers": [int(s["receivers"]) for s in stats],
+            "active": [int(s["active"]) for s in stats], "new_bits": [int(s["new_bits"]) for s in stats],
+            "digest_fp": _fp(dig), "coverage_fp": _fp(cov), "forwards_fp": fwd}
 
 
 def main():
@@ -317,13 +356,28 @@ def main():
         eng.set_message_shard(origin, None, lo, hi)
     else:
         eng.set_messages(origin)
+    # the N-GPU message-shard job combines its ranks' records into the job's
+    # (gp_shard_combine, csrc/shard.hip) over RCCL -- one GPU per rank -- or,
+    # when ranks share a GPU (a rehearsal on a smaller box: RCCL refuses two
+    # ranks per device), over the control plane's all-gather
+    job = shards and emu is None
+    if job:
+        if pkg._lib.device_count() >= world:
+            eng.shard_comm_init(dist.share_comm_id(pg, pkg.GossipEngine.comm_unique_id), world, rank)
+        else:
+            eng.shard_host_init(pg.all_gather_bytes, world, rank)
     setup_s += time.perf_counter() - t0
+    combine_ms = []
 
     def step():   # one whole gossip run, including the per-message coverage / forwards pass
         eng.reset()
         st = eng.run()
         eng.finalize()
-        return st
+        if job:   # the job's record, inside the step: every rank ends with the whole run's outputs
+            js, ms = eng.combine()
+            combine_ms.append(ms)
+            return st, js
+        return st, st
 
     for _ in range(args.warmup):
         step()
@@ -331,23 +385,26 @@ def main():
         pg.barrier()
     eng.synchronize()
     t0 = time.perf_counter()
-    runs = [step() for _ in range(args.steps)]
+    steps = [step() for _ in range(args.steps)]
     eng.synchronize()
     if pg is not None:
         pg.barrier()
     dt = dist.allmax(pg, time.perf_counter() - t0)
 
-    sends = sum(s["sends"] for r in runs for s in r)   # vertex partition: global (all-reduced) counters
+    # the whole run's counters: one GPU, the vertex partition (all-reduced every
+    # round) and the shard job (gp_shard_combine) all hold them
+    runs = [j for _, j in steps]
+    own_runs = [o for o, _ in steps]   # this rank's own rounds (its kernels)
+    sends = sum(s["sends"] for r in runs for s in r)
     rounds = sum(len(r) for r in runs)
-    if shards:   # message shards: every rank counted its own messages' deliveries
-        sends = int(dist.allsum(pg, [float(sends)])[0])
-        rounds = int(dist.allmax(pg, rounds))
-    exp_ms = sum(s["expand_ms"] for r in runs for s in r)
-    exch_ms = sum(s["exchange_ms"] for r in runs for s in r)
-    # roofline of the dominant kernel set, the pull: k_expand (or k_expand_flat)
-    # plus the hub passes that finish its hub receivers -- HIP events bracket
-    # all three (kernel_ms), and the algorithmic bytes count all three
-    pulls = [s for r in runs for s in r if s["mode"] == 0 and s["kernel_ms"] > 0]
+    own_rounds = sum(len(r) for r in own_runs)
+    exp_ms = sum(s["expand_ms"] for r in own_runs for s in r)
+    exch_ms = sum(s["exchange_ms"] for r in own_runs for s in r)
+    # roofline of the dominant kernel set, the pull: k_expand (or
+    # k_expand_flat), the hub passes that finish its hub receivers and, in
+    # degree-split rounds, the push half and the accumulator clear -- HIP events
+    # bracket all of them (kernel_ms), and the algorithmic bytes count all of them
+    pulls = [s for r in own_runs for s in r if s["mode"] == 0 and s["kernel_ms"] > 0]
     nbytes = sum(round_bytes(s, eng.words, n) for s in pulls)
     kern_ms = sum(s["kernel_ms"] for s in pulls)
     if world > 1 and not shards:   # counters are global (all-reduced): per-rank share for the per-GPU roofline
@@ -355,18 +412,22 @@ def main():
     achieved = nbytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     if shards:   # per-GPU roofline: mean over the ranks' own kernels
         achieved = float(dist.allsum(pg, [achieved])[0]) / world
-    dense_eq = dense_round_bytes(n, nnz, eng.words) * rounds / (1 if shards else world) / (exp_ms * 1e-3) / 1e9
+    dense_eq = dense_round_bytes(n, nnz, eng.words) * own_rounds / (1 if shards else world) / (exp_ms * 1e-3) / 1e9
     if args.profile_steps and rank == 0:
-        for s in runs[-1]:
+        for s in own_runs[-1]:
             print(json.dumps({k: s[k] for k in ("round", "mode", "new_bits", "sends", "active", "receivers",
                                                 "arcs_scanned", "rows_gathered", "seen_rows_read",
-                                                "rows_written", "row_bytes", "atomics", "done_nb", "lm_rows",
+                                                "rows_written", "row_bytes", "atomics", "done_nb", "lm_rows", "aliased",
                                                 "crashed", "reports", "removals", "scan", "expand_ms", "kernel_ms", "exchange_ms")}),
                   file=sys.stderr)
-    cpu = None
-    if rank == 0 and world == 1 and not emu and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, eng, origin, pkg)
+    record = job_record(eng, runs[-1], args.messages, job, world > 1 and not shards)
+    comm = None
+    if job:
+        cn, _, xp = eng.shard_info()
+        comm = {"transport": {1: "rccl", 2: "host all-gather (ranks share a GPU)"}.get(xp, "none"),
+                "comm_ranks": cn, "combine_ms_per_step": sum(combine_ms[-args.steps:]) / args.steps}
     if rank == 0:
+        split = " + the degree-split push half + k_acc_clear" if any(s["scan"] & 32 for s in pulls) else ""
         out = {
             "metric": f"gossip edge-deliveries/s (GTEPS) & HBM roofline %, 2^{args.log2n} nodes x {args.messages} msgs",
             "value": sends / dt / 1e9,
@@ -390,10 +451,15 @@ def main():
                        "edge_deliveries_per_step": sends // args.steps, "seed": args.seed,
                        "parallelism": (f"message-shard {emu[0]} of {emu[1]} alone (the per-GPU work of the "
                                        f"{emu[1]}-GPU run, {args.shard_assign})" if emu else
-                                       f"message-shard x{world} (no data-path collective, {args.shard_assign})"
+                                       f"message-shard x{world} ({args.shard_assign}), whole-job record combined "
+                                       f"in every step over {comm['transport']} (XOR reduce-scatter of the digests "
+                                       f"+ all-gather, OR reduce-scatter of the round bitmaps, all-gather of "
+                                       f"coverage / forwards / counters)"
                                        if shards else
                                        f"vertex-partition x{world}" + (" (sparse boundary exchange, ncclSend/Recv)"
                                                                       if world > 1 else "")),
+                       "comm": comm,
+                       "job": record,
                        "setup_s": round(setup_s, 2), "build_s": round(build_s, 2),
                        "degree_check": {"gamma_hat": round(deg["gamma_hat"], 4), "kmin": deg["kmin"],
                                         "gamma": args.gamma, "ok": bool(deg["ok"])}},
@@ -401,21 +467,26 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": (f"k_expand<{eng.words}> (+ k_mklm in line-mask rounds)" if eng.words > 32 else
                                     f"k_expand<{eng.words}> / k_expand_flat<{eng.words}>")
-                                   + " + k_hub_partial + k_hub_final per pull launch, HIP events on the "
-                                     "engine stream",
+                                   + " + k_hub_partial + k_hub_final" + split
+                                   + " per pull launch, HIP events on the engine stream",
                          "launches": len(pulls),
                          "avg_launch_ms": kern_ms / max(len(pulls), 1),
                          "alg_bytes_per_launch": nbytes / max(len(pulls), 1),
                          "expand_ms_per_step": exp_ms / args.steps,
                          "dense_equivalent_GBs": dense_eq,
-                         "exchange_ms_per_round": exch_ms / rounds},
-            "cpu_baseline": cpu,
+                         "exchange_ms_per_round": exch_ms / max(own_rounds, 1)},
+            "cpu_baseline": None,
         }
         traffic, src = pmc_traffic(out["config"])
         if traffic is not None:
             out["roofline"]["traffic"] = traffic
             out["roofline"]["traffic_source"] = src
             out["roofline"]["traffic_over_alg"] = traffic / out["roofline"]["alg_bytes_per_launch"]
+        if world == 1 and not emu and not args.no_cpu_baseline:
+            # the GPU line first (stderr), so that a CPU leg killed for memory
+            # does not take the measurement with it
+            print("gpu line (before cpu_baseline): " + json.dumps(out), file=sys.stderr, flush=True)
+            out["cpu_baseline"] = cpu_baseline(args, eng, origin, pkg)
         print(json.dumps(out), flush=True)
     eng.close()
     if pg is not None:

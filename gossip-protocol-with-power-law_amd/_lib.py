@@ -24,6 +24,12 @@ GP_OK, GP_EINVAL, GP_EHIP, GP_ENOMEM, GP_ESTATE, GP_ERCCL, GP_ENOTRACK = 0, -1, 
 
 # gp_what
 SEEN, FIRST, DIGEST, COVERAGE, FORWARDS, STATE, MISS, DEG_LIVE, ROW_PTR, COL, FRONTIER, FPOP, L2G = range(13)
+JOB_DIGEST, JOB_COVERAGE, JOB_FORWARDS = 13, 14, 15   # after gp_shard_combine
+# gp_shard_info transports
+XPORT_NONE, XPORT_RCCL, XPORT_HOST = 0, 1, 2
+
+# gp_allgather_fn: (user, send, bytes, recv[nranks * bytes]) -> 0 on success
+AllGatherFn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 
 
 class RoundStats(ctypes.Structure):
@@ -58,6 +64,7 @@ class RoundStats(ctypes.Structure):
         ("xchg_bytes", ctypes.c_uint64),
         ("done_nb", ctypes.c_uint64),
         ("lm_rows", ctypes.c_uint64),
+        ("aliased", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -125,12 +132,16 @@ SIGNATURES = {
     "gp_synchronize": (ctypes.c_int, [_P]),
     "gp_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI32, _PI32]),
     "gp_local_info": (ctypes.c_int, [_P, _PI64, _PI64, _PI64, _PI64, _PI64]),
+    "gp_shard_comm_init": (ctypes.c_int, [_P, _P, _I32, _I32]),
+    "gp_shard_host_init": (ctypes.c_int, [_P, AllGatherFn, _P, _I32, _I32]),
+    "gp_shard_info": (ctypes.c_int, [_P, _PI32, _PI32, _PI32]),
+    "gp_shard_combine": (ctypes.c_int, [_P, ctypes.POINTER(RoundStats), _I32, _PI32, ctypes.POINTER(ctypes.c_double)]),
     "gp_checkpoint_size": (ctypes.c_int, [_P, _PI64]),
     "gp_checkpoint_save": (ctypes.c_int, [_P, _P, _I64]),
     "gp_checkpoint_load": (ctypes.c_int, [_P, _P, _I64]),
 }
 
-ABI_VERSION = 17   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
+ABI_VERSION = 18   # include/gossip_capi.h GP_ABI_VERSION (struct layouts below)
 _lib = None
 
 

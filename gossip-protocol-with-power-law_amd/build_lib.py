@@ -13,7 +13,7 @@ OUT_DIR = os.path.join(PKG_DIR, "_build")
 LIB = os.path.join(OUT_DIR, "libgossip_hip.so")
 INCLUDE = os.path.join(os.path.dirname(PKG_DIR), "include", "gossip_capi.h")
 SOURCES = ["driver.hip", "setup.hip", "pull.hip", "hub.hip", "push.hip", "liveness.hip", "graph_build.hip",
-           "checkpoint.hip", "partition.hip", "bitcount.hip"]
+           "checkpoint.hip", "partition.hip", "bitcount.hip", "shard.hip"]
 HEADERS = ["gp_common.h", "gp_internal.h", "gp_device.h", "xplan.h"]
 ARCH = os.environ.get("GOSSIP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", f"--offload-arch={ARCH}"]

@@ -411,6 +411,7 @@ int bitcount_messages(Ctx* c, bool weighted, u64* cov, u64* fwd) {
   int64_t n = c->nloc();
   if (weighted && (u64)c->nnz_l >= (1ull << 32))
     return set_error(GP_EINVAL, "bitcount: per-block weighted sums are 32-bit (arcs < 2^32)");
+  GP_TRY(unalias(c, false));   // (this pass reads every row, complete ones too)
   if (weighted) GP_TRY(bc_keys(c));
   const int64_t n_all = n;
   if (weighted) n = c->bc_split;   // the tail is counted by k_bitcount_tail

@@ -115,6 +115,7 @@ int gp_checkpoint_save(gp_ctx* c, void* host, int64_t bytes) {
   if (bytes != blob_bytes(c, nrep))
     return set_error(GP_EINVAL, "bytes mismatch: expected " + std::to_string(blob_bytes(c, nrep)));
   GP_HIP(hipSetDevice(c->device));
+  GP_TRY(unalias(c, false));   // aliased Message-Lists are saved as the rows they stand for
   GP_HIP(hipStreamSynchronize(c->stream));
   uint8_t* out = static_cast<uint8_t*>(host);
   CkptHeader h{};
@@ -227,6 +228,11 @@ int gp_checkpoint_load(gp_ctx* c, const void* host, int64_t bytes) {
   }
   c->liveness_active = h.liveness_active != 0;
   c->alive_from = h.alive_from1 - 1;
+  // a blob written before the field was alive_from + 1 holds 0 there; current
+  // code never saves an active liveness phase without a complete alive set
+  // from some round, so 0 with liveness on means "unknown": the alive set the
+  // next round builds is complete from the round after it (as after gp_crash)
+  if (h.alive_from1 == 0 && c->liveness_active) c->alive_from = c->round + 1;
   c->pending_crash = h.pending_crash != 0;
   c->msg_forwards_valid = h.msg_forwards_valid != 0;
   c->done_dirty = true;   // the working targets came from the blob; the next reset restores the pristine ones

@@ -332,6 +332,8 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.midx = c->d_midx;
   a.cmask = c->d_cmask;
   a.early_exit = c->early_exit_now ? 1 : 0;
+  a.dprobe = c->dprobe_now ? 1 : 0;
+  a.alias = c->alias_now ? 1 : 0;
   a.fpop_next = c->d_fpop[c->cur ^ 1];
   a.seenpop = c->d_seenpop;
   a.first = c->cfg.track_first ? c->d_first : nullptr;
@@ -466,6 +468,21 @@ static int launch_expand(Ctx* c) {
       !c->local && c->nloc() == c->n_alloc && c->words > c->cfg.flat_max_words && c->sate_since >= 0 &&
       c->round > c->sate_since)
     c->dnb_now = true;
+  // aliased Message-Lists (W = 64, no liveness, one context,
+  // no compact records): in done-neighbour rounds every arc the pull scans
+  // probes the done bitmap (a receiver with any done in-neighbour takes its
+  // target) and receivers that complete commit SLOT_CMASK instead of a
+  // 512-B row.  Once a run holds aliases every later pull is such a round
+  // (held bits only grow, so early exit and the done bitmap stay on), and a
+  // push round first writes its aliased senders' rows (k_unalias)
+  const bool alias_ok = c->words == 64 && !c->liveness_active && !c->local && c->nloc() == c->n_alloc &&
+                        c->cfg.compact_rows == 0 && c->words > c->cfg.flat_max_words;
+  c->dprobe_now = c->dnb_now && alias_ok;
+  c->alias_now = c->dprobe_now;
+  if (c->alias_active) {
+    if (c->mode_push) GP_TRY(unalias(c, true));
+    else if (!c->dprobe_now) GP_TRY(unalias(c, false));   // (a pull that could gather a done sender's row)
+  }
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8 * GS))),
                      dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc,
                      c->d_seenpop, c->d_done_at, c->dnb_now ? c->d_dbits : nullptr,
@@ -533,6 +550,10 @@ static int launch_expand(Ctx* c) {
     c->split_now = row > 0 && row + c->nloc() <= (int64_t)INT32_MAX;
     c->acc_row = (int32_t)row;
   }
+  if (c->dprobe_now) {   // the scan modes whose gathers probe the done bitmap: filtered and unfiltered
+    c->arc_mask_now = c->prefilter_now = c->split_now = false;
+    c->cml_read_now = c->cml_write_now = c->lines_now = c->lm_write_now = false;
+  }
   if (narrow_split && !c->split_now)   // (the conditions above mirror these: a pull was promised a split)
     return set_error(GP_ESTATE, "internal: narrow-row split round not eligible");
   if (c->split_now) GP_TRY(build_prehi(c, c->cfg.split_deg));
@@ -597,6 +618,7 @@ static int round_launch(Ctx* c) {
 
   auto it = c->inject.find(r);
   if (it != c->inject.end() && it->second.cnt > 0) {
+    GP_TRY(unalias(c, false));   // (k_inject reads the origins' rows; no vertex completes before the last injection)
     InjectArgs ia{};
     ia.origin = c->d_inj_origin;
     ia.bits = c->d_inj_bits;
@@ -686,7 +708,9 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   if (h[S_XERR])   // (every rank of an RCCL partition sees the all-reduced count)
     return set_error(GP_ERCCL, "boundary exchange: " + std::to_string(h[S_XERR]) +
                                    " received entries do not match the exchange plan (round " + std::to_string(r) + ")");
-  if (out) {
+  gp_round_stats own;
+  {
+    gp_round_stats* out = &own;   // (kept for the run: a shard job's combine reads it)
     std::memset(out, 0, sizeof(*out));
     out->round = r;
     out->injected = h[S_INJECTED];
@@ -710,7 +734,8 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->mode = c->mode_push ? 1 : 0;
     out->scan = c->mode_push ? 0 : (c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : c->prefilter_now ? 3 : 0) |
                                        (c->cml_read_now ? 4 : 0) | (c->lines_ran ? 8 : 0) |
-                                       (c->lines_from_commits ? 16 : 0) | (c->split_now ? 32 : 0);
+                                       (c->lines_from_commits ? 16 : 0) | (c->split_now ? 32 : 0) |
+                                       (c->dprobe_now ? 64 : 0);
     out->kernel_ms = 0.0;
     if (!c->mode_push && c->nloc() > 0) {
       float kms = 0.f;
@@ -722,6 +747,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->xchg_bytes = h[S_XBYTES];
     out->done_nb = h[S_DNB];
     out->lm_rows = h[S_LM_ROWS];
+    out->aliased = h[S_ALIASED];
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, c->ev[1], c->ev[2]);
     out->expand_ms = ms;
@@ -730,6 +756,8 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[3]);
     out->round_ms = ms;
   }
+  if (out) *out = own;
+  c->run_stats.push_back(own);
   c->last_reports = (int64_t)h[S_REPORT_CURSOR];
   c->prev_next_arcs = h[S_NEXT_ARCS];
   c->prev_new_bits = h[S_NEW_BITS];
@@ -737,6 +765,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   c->held_bits += h[S_INJECTED] + h[S_NEW_BITS];
   c->cml_written_prev = c->cml_write_now;
   c->lm_written_prev = c->lm_write_now;
+  if (h[S_ALIASED]) c->alias_active = true;
   c->cur ^= 1;
   c->round = r + 1;
   return 0;
@@ -772,6 +801,7 @@ int gp_round(gp_ctx* c, gp_round_stats* out) {
     return set_error(GP_ESTATE, "a partitioned context exchanges over RCCL (gp_comm_init) or in gp_round_group");
   GP_TRY(round_launch(c));
   GP_TRY(round_exchange_rccl(c));
+  if (c->jnranks > 0) GP_TRY(shard_record_round(c));   // (message-shard job: shard.hip)
   return round_collect(c, out);
 }
 
@@ -872,6 +902,7 @@ int gp_finalize_messages(gp_ctx* c) {
     GP_HIP(hipMemcpyAsync(gfwd, fwd_local, M * 8, hipMemcpyDeviceToDevice, s));
   }
   GP_HIP(hipStreamSynchronize(s));
+  c->fin_round = c->round;
   return 0;
 }
 
@@ -891,6 +922,7 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
     case GP_SEEN:
       if (!run) return set_error(GP_ESTATE, "no run state");
       GP_TRY(need(nl * W * 8));
+      GP_TRY(unalias(c, false));   // (aliased Message-Lists become rows of S[cur])
       if (bytes) {   // owned rows of every slot, picked per vertex by its slot byte
         // blocks of rows: host scratch stays at 2 blocks whatever n (a 2^26 x
         // 4096 read would otherwise hold two more 32 GiB copies)
@@ -972,6 +1004,23 @@ int gp_read(gp_ctx* c, int32_t what, void* host, int64_t bytes) {
         for (int64_t v = 0; v < c->n; ++v) static_cast<int32_t*>(host)[v] = (int32_t)v;
       }
       return 0;
+    case GP_JOB_DIGEST:
+    case GP_JOB_COVERAGE:
+    case GP_JOB_FORWARDS: {   // the job record of gp_shard_combine (shard.hip)
+      if (!c->j_ready) return set_error(GP_ESTATE, "gp_shard_combine first");
+      if (what == GP_JOB_DIGEST) {
+        if (!c->j_dig_valid) return set_error(GP_ENOTRACK, "track_digest is off");
+        GP_TRY(need(c->n * 8));
+        GP_TRY(copy_sync(c, host, c->d_jdig, (size_t)bytes, hipMemcpyDeviceToHost));
+        return 0;
+      }
+      if (what == GP_JOB_FORWARDS && !c->j_fwd_valid)
+        return set_error(GP_ENOTRACK, "churn run without track_msg_forwards (on some rank)");
+      GP_TRY(need((int64_t)c->jm * 8));
+      GP_TRY(copy_sync(c, host, c->d_jcf + (what == GP_JOB_COVERAGE ? 0 : (size_t)c->jm), (size_t)bytes,
+                       hipMemcpyDeviceToHost));
+      return 0;
+    }
 #ifdef GP_DBG_READ   // scripts/debug_mask2.py: arc mask, gather-order columns, activity bits
     case 100:
       GP_TRY(copy_sync(c, host, c->d_amask, (size_t)bytes, hipMemcpyDeviceToHost));

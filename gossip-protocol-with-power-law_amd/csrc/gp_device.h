@@ -152,6 +152,10 @@ struct ExpandArgs {
   const int32_t* __restrict__ midx;    // [n] row of v's component in cmask (-1: no messages)
   const u64* __restrict__ cmask;       // [K][W] messages originating in each component
   int32_t early_exit;                  // this round scans with the coverage check
+  int32_t dprobe;                      // early exit + dbits (W = 64 pulls): every scanned arc probes the done
+                                       //   bitmap first; a done in-neighbour anywhere makes the receiver's
+                                       //   new bits its target (done_nb's rule) -- no aliased row is gathered
+  int32_t alias;                       // dprobe rounds: receivers that complete commit SLOT_CMASK, no row
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
   int32_t near_done;                   // early-exit round with most messages held: fewer rows in flight
   const u64* __restrict__ alive;       // [W] messages some sender forwards this round (or null)
@@ -211,6 +215,14 @@ struct ExpandArgs {
 
 constexpr uint8_t SLOT_NONE = 0xFF;
 constexpr uint8_t SLOT_PARKED = 2;   // row in d_slot[2] (a down vertex, before an unfiltered pull)
+// aliased Message-List: v completed its component in a dprobe
+// round without liveness, so its Message-List is cmask[midx[v]] and no row was
+// written.  Only dprobe pulls run while a context holds aliases (they never
+// gather a done sender's row); every other reader materializes them first
+// (k_unalias)
+constexpr uint8_t SLOT_CMASK = 3;
+// commit flag beside the 4-bit line mask in the deferred per-vertex words
+constexpr uint8_t LMN_ALIAS = 0x10;
 
 // Message-List records (W = 64): a round whose receivers end
 // up with sparse Message-Lists also writes, per receiver, a 128-B record --
@@ -661,8 +673,20 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
       wave_sync_lds();
       cnt = __popcll(win);
     } else {
-      int32_t ent = -1;
-      if (lane < n) ent = probe<MODE>(a, (col0 != INT32_MIN && j0 == b) ? col0 : a.gcol[j0 + lane]);
+      int32_t ent = -1, u = -1;
+      u64 dw = 0;
+      if (lane < n) {
+        u = (col0 != INT32_MIN && j0 == b) ? col0 : a.gcol[j0 + lane];
+        if (a.dprobe) dw = a.dbits[u >> 6];   // (beside the activity probe: one round trip)
+        ent = probe<MODE>(a, u);
+      }
+      // a done in-neighbour in this pass: the receiver's new bits are its
+      // whole target (done_nb's rule, any arc), and none of the pass's rows
+      // is gathered -- an aliased sender's row slot holds no Message-List
+      if (a.dprobe && __any(u >= 0 && ((dw >> (u & 63)) & 1ull))) {
+        acc = want;
+        break;
+      }
       cnt = stage_pass(L, ent);
       if (cnt == 0) continue;
     }
@@ -730,10 +754,13 @@ __device__ __forceinline__ void set_dense(u64* __restrict__ bm, int v) {
 // go to L.tot/L.dig[k] and the wave commits them for its 64 vertices at once,
 // coalesced, after its loop -- one scattered read-modify-write chain less per
 // receiver, and whole cache lines instead of 1-8 byte pieces.
+// alias (DEFER, a.alias rounds): the receiver completes its component this
+// round (acc covers its early-exit target), so its new Message-List is its
+// component row: no row is written, the commit sets SLOT_CMASK
 template <int W, bool DEFER = false, bool CMLW = true, class LDS = WaveLds>
 __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i, u64x2 acc, int lane,
                                            int g, int lw, WaveStats& st, LDS& L, bool have_sv,
-                                           uint32_t sv_slot, int k = 0) {
+                                           uint32_t sv_slot, int k = 0, bool alias = false) {
   constexpr int WPL = Geo<W>::WPL;
   const bool nz = (acc.x | acc.y) != 0;
   if (!__any(nz)) {
@@ -771,7 +798,7 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   }
   if (g == 0) {
     alive_add<W>(a, L, lw, nw);
-    store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);   // the whole row: the slot may hold an older one
+    if (!alias) store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);   // the whole row: the slot may hold an older one
     if (a.frx_next) store_piece<W>(a.frx_next, v, lw, nw);
     if (a.first) {
       uint8_t* row = a.first + (size_t)i * (W * 64);
@@ -795,7 +822,7 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   if constexpr (DEFER) {
     if (lane == 0) {
       L.tot[k] = tot;
-      L.lmn[k] = (uint8_t)lmn;
+      L.lmn[k] = (uint8_t)lmn | (alias ? LMN_ALIAS : (uint8_t)0);
       if constexpr (CMLW && LDS::kCml) L.cd[k] = dense ? 1 : 0;
     }
   } else {
@@ -812,7 +839,7 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
   }
   st.add(S_NEW_BITS, tot);
   st.add(S_RECEIVERS, 1);
-  st.add(S_WRITTEN, 1);
+  st.add(alias ? S_ALIASED : S_WRITTEN, 1);
 }
 
 // k_expand's commit of the deferred per-vertex words: lane k holds vertex
@@ -829,15 +856,19 @@ __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, LDS& L, int
     a.fpop_next[v] = tot;
     if (tot) {
       a.seenpop[li] += tot;
-      a.sp[v] = (uint8_t)a.wslot;
-      a.ws[v] |= (uint8_t)(1u << a.wslot);
+      if (L.lmn[lane] & LMN_ALIAS) {
+        a.sp[v] = SLOT_CMASK;
+      } else {
+        a.sp[v] = (uint8_t)a.wslot;
+        a.ws[v] |= (uint8_t)(1u << a.wslot);
+      }
       if (a.digest) a.digest[li] ^= L.dig[lane];
       next_arcs = (u64)(uint32_t)max(a.deg_live[v], 0);
     }
   }
   st.add(S_NEXT_ARCS, wave_sum_u64(next_arcs));
   if (a.lm_next) {   // line masks of the next round's senders, two vertices per byte (hubs: 0 here)
-    const uint32_t nib = (need && L.tot[lane]) ? (uint32_t)L.lmn[lane] : 0u;
+    const uint32_t nib = (need && L.tot[lane]) ? (uint32_t)(L.lmn[lane] & 0xF) : 0u;
     const uint32_t hi = (uint32_t)__shfl_xor((int)nib, 1);
     if (!(lane & 1) && li < a.nloc) a.lm_next[li >> 1] = (uint8_t)(nib | (hi << 4));
   }

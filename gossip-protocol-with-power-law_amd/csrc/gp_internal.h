@@ -26,11 +26,12 @@ enum StatSlot {
   S_XROWS, S_XBYTES,   // boundary entries / bytes sent (vertex partition, written by the pack step)
   S_DNB,               // receivers completed from a done in-neighbour (k_expand)
   S_LM_ROWS,           // senders' rows read by k_mklm to build line masks
+  S_ALIASED,           // receivers committed as an alias of their component row (no row write, §3.2)
   NST,
   // boundary entries the unpack found inconsistent with the exchange plan
   // (partition.hip k_rx_unpack); all-reduced with the counters, fails the round
   S_XERR = NST + 1,
-  S_REPORT_CURSOR = 24, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR, S_DET_BIG
+  S_REPORT_CURSOR = 26, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR, S_DET_BIG
 };
 static_assert(S_XERR < S_REPORT_CURSOR, "S_XERR must be inside the all-reduced counter slots");
 
@@ -170,6 +171,14 @@ struct Ctx {
   // line-mask variant, and with masks the previous round's commits wrote
   bool lines_ran = false, lines_from_commits = false;
   bool split_now = false;   // degree-split round: low-degree senders push, receivers probe a prefix
+  // aliased Message-Lists: a receiver that completes its
+  // component in a W = 64 early-exit pull writes no row; sp = SLOT_CMASK says
+  // its Message-List is cmask[midx[v]].  dprobe_now: the pull probes the done
+  // bitmap for every arc it scans (a receiver with any done in-neighbour takes
+  // its target and gathers nothing, so an aliased row is never gathered);
+  // alias_now: its complete receivers alias; alias_active: the run holds
+  // aliases (readers of rows outside such pulls materialize them, k_unalias)
+  bool dprobe_now = false, alias_now = false, alias_active = false;
   int32_t acc_row = 0;      // its accumulator rows addressed as rows of the round's slot buffer
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
   u64* d_amask = nullptr;
@@ -255,6 +264,24 @@ struct Ctx {
   // rccl
   ncclComm_t comm = nullptr;
 
+  // message-shard job (shard.hip): jnranks > 0 once a transport
+  // is set; the rounds then record the receiver / sender bitmaps of the run
+  ncclComm_t jcomm = nullptr;           // gp_shard_comm_init
+  gp_allgather_fn jhost = nullptr;      // gp_shard_host_init
+  void* jhost_user = nullptr;
+  int32_t jrank = 0, jnranks = 0;
+  u64* d_hist = nullptr;                // [hist_cap][2][nwords]: round r's receivers, then senders
+  int32_t hist_cap = 0, hist_rounds = 0;
+  std::vector<gp_round_stats> run_stats;   // this run's rounds, as gp_round returned them
+  int32_t fin_round = -1;               // round count at the last gp_finalize_messages of this run
+  u64* d_jscr = nullptr;                // combine scratch (send / receive chunks)
+  size_t jscr_words = 0;
+  u64* d_jdig = nullptr;                // [P * ceil(n / P)] the job's digest (first n valid)
+  size_t jdig_words = 0;
+  u64* d_jcf = nullptr;                 // [2][jm] the job's coverage, forwards
+  int32_t jm = 0;                       // messages of the job
+  bool j_ready = false, j_fwd_valid = false, j_dig_valid = false;
+
   // kernel geometry
   int cu_count = 256;
 
@@ -322,6 +349,13 @@ int alloc_exchange(Ctx* c);                    // exchange buffers for the curre
 int pack_boundary(Ctx* c);                     // after E_r: this round's boundary entries -> send buffers
 int exchange_rccl(Ctx* c);                     // counts, rows, alive sets over RCCL, then unpack
 int exchange_group(Ctx** ctxs, int32_t nctx);  // the same through device-to-device copies
+// pull.hip: write the component rows of aliased vertices (all, or this
+// round's senders only) into S[cur]; with all, the run holds no alias after
+int unalias(Ctx* c, bool senders_only);
+// shard.hip
+int shard_record_round(Ctx* c);                // after E_r of a shard job: round r's bitmaps
+void shard_free(Ctx* c);
+void shard_reset(Ctx* c);                      // new run (gp_reset, checkpoint load)
 // state bit: removed by this rank's seed step in the current round (sent to the
 // ranks holding the vertex as a ghost; cleared by the next round's k_churn)
 constexpr uint8_t ST_RMNEW = 8;

@@ -1,7 +1,13 @@
 // hub.hip -- hub receivers of the pull (hub load balancing):
 // vertices above hub_threshold in-arcs are split over waves, each wave ORs one
 // chunk of the in-list into a partial row (k_hub_partial), k_hub_final combines
-// a hub's partials and commits the row.  Deterministic, no atomics on rows.
+// a hub's partials and commits the row.  No atomics on rows, and the rows are
+// deterministic: every chunk's OR is a subset of the hub's new bits, so the OR
+// of the partials is exact whichever chunks stopped early.  The work counters
+// are not: in early-exit rounds a chunk that covers the hub's target stamps
+// hub_done and the hub's other chunks stop at their next 512 arcs, so
+// arcs_scanned / rows_gathered / row_bytes of such rounds depend on wave
+// timing ("Counters").
 #include "gp_device.h"
 
 namespace gp {

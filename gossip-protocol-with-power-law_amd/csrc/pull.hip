@@ -23,9 +23,12 @@ namespace gp {
 
 // receiver side of a pair: half h holds receiver ks (on: the half has one;
 // kB < 0: half 1 idle) with its gathered OR acc and its seen row sv
+// (alias: both receivers complete their component -- done in-neighbours in an
+// a.alias round -- and commit SLOT_CMASK instead of a row, finish_row)
 template <int W, class LDS>
 __device__ __forceinline__ void pair_finish(const ExpandArgs& a, LDS& L, int h, int lw, bool on, int ks, int kB,
-                                            int64_t i, int v, u64x2 acc, u64x2 sv, WaveStats& st) {
+                                            int64_t i, int v, u64x2 acc, u64x2 sv, WaveStats& st,
+                                            bool alias = false) {
   const u64x2 nw = acc & ~sv;
   uint32_t tot = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
 #pragma unroll
@@ -49,7 +52,7 @@ __device__ __forceinline__ void pair_finish(const ExpandArgs& a, LDS& L, int h, 
   }
   if (on && tot) {
     alive_add<W>(a, L, lw, nw);
-    store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);
+    if (!alias) store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);
     if (a.frx_next) store_piece<W>(a.frx_next, v, lw, nw);
     if (a.first) {
       uint8_t* row = a.first + (size_t)i * (W * 64);
@@ -67,7 +70,7 @@ __device__ __forceinline__ void pair_finish(const ExpandArgs& a, LDS& L, int h, 
   if (a.lm_next) lmn = lines_of((uint32_t)(__ballot(on && (nw.x | nw.y) != 0ull) >> (32 * h)));
   if (lw == 0 && on && tot) {
     L.tot[ks] = tot;
-    L.lmn[ks] = (uint8_t)lmn;
+    L.lmn[ks] = (uint8_t)lmn | (alias ? LMN_ALIAS : (uint8_t)0);
     L.dig[ks] = t;
     if constexpr (LDS::kCml) L.cd[ks] = dense ? 1 : 0;
   }
@@ -75,7 +78,7 @@ __device__ __forceinline__ void pair_finish(const ExpandArgs& a, LDS& L, int h, 
   const uint32_t tB = kB >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)tot, 32) : 0u;
   st.add(S_NEW_BITS, (u64)tA + (u64)tB);
   st.add(S_RECEIVERS, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
-  st.add(S_WRITTEN, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
+  st.add(alias ? S_ALIASED : S_WRITTEN, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
 }
 
 // the seen row of a pair's receivers, loaded after a gather without early
@@ -190,7 +193,7 @@ __device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
     const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
     st.add(S_SEEN_READ, (u64)((sA != SLOT_NONE ? 1 : 0) + (kB >= 0 && sB != SLOT_NONE ? 1 : 0)));
-    pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, cm, sv, st);
+    pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, cm, sv, st, !ALIVE && a.alias != 0);
   }
 }
 
@@ -453,7 +456,15 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
           wave_sync_lds();
         }
       }
-      finish_row<W, true, (MODE & SCAN_CML) != 0>(a, v, i, acc, lane, g, lw, st, L, ee || SEEN_EARLY, sv_slot, k);
+      // alias rounds: a receiver whose gather covered its whole target now
+      // holds its component's row (no liveness: want = cm & ~seen)
+      bool full = false;
+      if (!ALIVE && a.alias && ee) {
+        const u64x2 rem = want & ~acc;
+        full = !__any((rem.x | rem.y) != 0ull);
+      }
+      finish_row<W, true, (MODE & SCAN_CML) != 0>(a, v, i, acc, lane, g, lw, st, L, ee || SEEN_EARLY, sv_slot, k,
+                                                  full);
     }
     alive_flush<W>(a, L.alive, lane);
     commit_vertices(a, L, li, need, st);
@@ -1136,6 +1147,43 @@ __global__ __launch_bounds__(BLOCK) void k_arcmask(const int32_t* __restrict__ g
 // whose slot was not written this run hold data of an earlier run: zero them.
 // One wave per 64-vertex bitmap word; fully active words cost two loads.
 // (Only without liveness: a crashed vertex may hold bits it never sent.)
+// Materialize aliased Message-Lists (SLOT_CMASK): write the
+// component row of every aliased vertex (with fpop: of this round's senders
+// only, before a push round reads them) into S[cur] and point sp there.  One
+// wave per 64 vertices, a row per aliased vertex in one coalesced store.
+__global__ __launch_bounds__(BLOCK) void k_unalias(uint8_t* __restrict__ sp, uint8_t* __restrict__ ws,
+                                                   const uint32_t* __restrict__ fpop, const int32_t* __restrict__ midx,
+                                                   const u64* __restrict__ cmask, u64* __restrict__ rows,
+                                                   int32_t cur, int64_t n, int32_t W) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6); w * 64 < n; w += (int64_t)gridDim.x * WAVES) {
+    const int64_t v = w * 64 + lane;
+    const bool al = v < n && sp[v] == SLOT_CMASK && (!fpop || fpop[v] != 0u);
+    u64 todo = __ballot(al);
+    if (al) {
+      sp[v] = (uint8_t)cur;
+      ws[v] |= (uint8_t)(1u << cur);
+    }
+    while (todo) {
+      const int b = __ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const int64_t u = w * 64 + b;
+      const int32_t k = midx[u];
+      if (lane < W) rows[(size_t)u * W + lane] = cmask[(size_t)k * W + lane];
+    }
+  }
+}
+
+int unalias(Ctx* c, bool senders_only) {
+  if (!c->alias_active) return 0;
+  hipLaunchKernelGGL(k_unalias, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8 * GS)),
+                     dim3(BLOCK), 0, c->stream, c->d_sp, c->d_ws, senders_only ? c->d_fpop[c->cur] : nullptr,
+                     c->d_midx, c->d_cmask, c->d_slot[c->cur], c->cur, c->n_alloc, c->words);
+  GP_HIP(hipGetLastError());
+  if (!senders_only) c->alias_active = false;
+  return 0;
+}
+
 template <int W>
 __global__ __launch_bounds__(BLOCK) void k_fixup_rows(const u64* __restrict__ abits, uint8_t* __restrict__ ws,
                                                       u64* __restrict__ rows, int32_t rslot, int64_t n_alloc) {

@@ -511,6 +511,7 @@ void gp_destroy(gp_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  shard_free(c);
   dfree(&c->d_row_ptr); dfree(&c->d_col); dfree(&c->d_out_row_ptr); dfree(&c->d_out_col);
   dfree(&c->d_deg_out); dfree(&c->d_comp); dfree(&c->d_abits); dfree(&c->d_dbits); dfree(&c->d_lm); dfree(&c->d_lmw[0]); dfree(&c->d_lmw[1]); dfree(&c->d_sbits); dfree(&c->d_amask); dfree(&c->d_cml[0]); dfree(&c->d_cml[1]); dfree(&c->d_cmk[0]); dfree(&c->d_cmk[1]); dfree(&c->d_done_at);
   dfree(&c->d_done_at0); dfree(&c->d_cmask0); dfree(&c->d_lostcnt); dfree(&c->d_alive);
@@ -820,6 +821,8 @@ int gp_reset(gp_ctx* c) {
   c->pending_crash = false;
   c->msg_forwards_valid = true;
   c->last_reports = 0;
+  c->alias_active = c->alias_now = c->dprobe_now = false;
+  shard_reset(c);
   GP_HIP(hipStreamSynchronize(s));
   return 0;
 }
@@ -832,6 +835,7 @@ int gp_crash(gp_ctx* c, int32_t nverts, const int32_t* verts) {
     if (verts[k] < 0 || verts[k] >= c->n) return set_error(GP_EINVAL, "vertex out of range");
   // global ids; a partitioned context applies the crashes of the vertices it
   // holds (owned, ghosts, origins) -- the others never touch its slice
+  GP_TRY(unalias(c, false));   // (liveness turns on: the run's rounds can no longer keep aliases)
   std::vector<uint8_t> st((size_t)c->n_alloc);
   GP_HIP(hipStreamSynchronize(c->stream));
   GP_TRY(copy_sync(c, st.data(), c->d_state, (size_t)c->n_alloc, hipMemcpyDeviceToHost));

@@ -151,6 +151,56 @@ class GossipEngine:
         buf = ctypes.create_string_buffer(bytes(unique_id), 128)
         check(self._lib.gp_comm_init(self._ctx, buf, int(nranks), int(rank)))
 
+    # -- message-shard jobs (csrc/shard.hip) -----------------
+    def shard_comm_init(self, unique_id, nranks, rank):
+        """Join an nranks-rank message-shard job over RCCL (one GPU per rank;
+        rank 0 makes the id with comm_unique_id())."""
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        check(self._lib.gp_shard_comm_init(self._ctx, buf, int(nranks), int(rank)))
+
+    def shard_host_init(self, all_gather_bytes, nranks, rank):
+        """Join a message-shard job whose combine moves its chunks through the
+        host: all_gather_bytes(bytes) -> [bytes of rank 0, ..., rank nranks-1]
+        (ranks sharing a GPU, which RCCL refuses)."""
+        def fn(_user, send, nbytes, recv):
+            try:
+                parts = all_gather_bytes(ctypes.string_at(send, nbytes))
+                if len(parts) != nranks or any(len(p) != nbytes for p in parts):
+                    return -1
+                ctypes.memmove(recv, b"".join(parts), nranks * nbytes)
+                return 0
+            except Exception:   # (a C caller cannot take a Python exception)
+                return -1
+        self._shard_cb = _lib.AllGatherFn(fn)   # kept alive as long as the context
+        check(self._lib.gp_shard_host_init(self._ctx, self._shard_cb, None, int(nranks), int(rank)))
+
+    def shard_info(self):
+        """(nranks, rank, transport) as the job's transport reports them:
+        ncclCommCount / ncclCommUserRank for RCCL (transport 1), the host
+        all-gather's (2), or (0, 0, 0) outside a shard job."""
+        v = [ctypes.c_int32() for _ in range(3)]
+        check(self._lib.gp_shard_info(self._ctx, *[ctypes.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
+    def combine(self, max_rounds=254):
+        """gp_shard_combine after run(): the job's per-round counters (list of
+        dicts, every rank the same) and the combine's device time in ms.  The
+        job's digest / coverage / forwards are then job_digest() etc."""
+        buf = (_lib.RoundStats * max_rounds)()
+        k = ctypes.c_int32()
+        ms = ctypes.c_double()
+        check(self._lib.gp_shard_combine(self._ctx, buf, int(max_rounds), ctypes.byref(k), ctypes.byref(ms)))
+        return [buf[i].as_dict() for i in range(k.value)], ms.value
+
+    def job_digest(self):
+        return self._read(_lib.JOB_DIGEST, np.empty(self.n, dtype=np.uint64))
+
+    def job_coverage(self, m_total):
+        return self._read(_lib.JOB_COVERAGE, np.empty(int(m_total), dtype=np.uint64))
+
+    def job_forwards(self, m_total):
+        return self._read(_lib.JOB_FORWARDS, np.empty(int(m_total), dtype=np.uint64))
+
     # -- messages / run ----------------------------------------------------
     def set_messages(self, origin, inject_round=None):
         o = np.ascontiguousarray(origin, dtype=np.int32)

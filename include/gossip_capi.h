@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GP_ABI_VERSION 17
+#define GP_ABI_VERSION 18
 
 typedef struct gp_ctx gp_ctx;
 
@@ -91,7 +91,9 @@ typedef struct gp_round_stats {
                                the previous round's commits (no k_mklm pass);
                                + 32: degree-split round (senders of in-degree <
                                split_deg pushed, receivers probe the gather-order
-                               prefix of the others, §3.2)                        */
+                               prefix of the others, §3.2); + 64: every scanned
+                               arc probed the done bitmap (complete receivers
+                               alias their component row, `aliased`, §3.2)        */
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
@@ -103,6 +105,9 @@ typedef struct gp_round_stats {
                                from an in-neighbour holding all of them (§3.4)      */
   uint64_t lm_rows;         /* senders' rows read to build line masks before a
                                filtered 64-word pull (8*W bytes each, §3.2)         */
+  uint64_t aliased;         /* receivers that completed their component and took it
+                               as their Message-List without writing a row (their
+                               slot byte names the component row, §3.2; ABI 18)    */
 } gp_round_stats;
 
 /* One dead-node report: reporter saw `dead` miss 3 heartbeats in `round`. */
@@ -174,8 +179,12 @@ typedef enum gp_what {
   GP_FRONTIER = 10,   /* u64 [n][W] current frontier (rows with FPOP==0 read as 0);
                          kept only with track_msg_forwards (else GP_ENOTRACK)      */
   GP_FPOP = 11,       /* u32 [n] |frontier(v)|                                       */
-  GP_L2G = 12         /* i32 [local slots] global id of each local vertex (identity
+  GP_L2G = 12,        /* i32 [local slots] global id of each local vertex (identity
                          unless partitioned: owned, then ghosts, then origin extras) */
+  /* the whole job of a message-shard run, after gp_shard_combine (else GP_ESTATE) */
+  GP_JOB_DIGEST = 13,   /* u64 [n]        per-vertex digest of every shard's messages    */
+  GP_JOB_COVERAGE = 14, /* u64 [m_total]  vertices holding message k of the job table    */
+  GP_JOB_FORWARDS = 15  /* u64 [m_total]  sends of message k (GP_ENOTRACK as GP_FORWARDS) */
 } gp_what;
 
 int gp_abi_version(void);
@@ -246,6 +255,37 @@ int gp_info(gp_ctx* ctx, int64_t* n, int64_t* nnz, int32_t* m, int32_t* words);
  * extras, arcs of the local CSR, boundary entries it sends to (all peers). */
 int gp_local_info(gp_ctx* ctx, int64_t* nloc, int64_t* nghost, int64_t* nextra, int64_t* nnz_local,
                   int64_t* n_boundary);
+
+/* Message-shard jobs.  Messages never interact, so an N-GPU
+ * job runs one context per GPU on the whole overlay, rank p holding the
+ * word-aligned block of the message table that starts at global word
+ * gp_config.msg_word_base.  The reference keeps each peer's whole receive
+ * record (Peer.py:175-216); gp_shard_combine makes the job's record out of the
+ * ranks' after gp_run: the per-vertex digests XOR-reduced (reduce-scatter by
+ * ncclSend/ncclRecv of 1/N vertex slices + an XOR kernel, then ncclAllGather),
+ * the per-message coverage / forwards all-gathered into the job's message
+ * order, and the per-round counters: additive ones summed, `receivers` and
+ * `active` as the popcount of the OR of the ranks' per-round vertex bitmaps
+ * (reduce-scattered like the digests: a vertex receiving in two shards counts
+ * once), liveness counters checked equal across ranks.  Every rank gets the
+ * same job record.
+ *
+ * The transport is a communicator of the shard ranks (gp_shard_comm_init: one
+ * GPU per rank), or the host's own all-gather (gp_shard_host_init: ranks
+ * sharing a GPU, which RCCL refuses -- the rehearsal of a one-GPU box; the
+ * reductions still run on the device).  Rounds of a shard job take no
+ * collective: each rank decides its own direction / scan modes.  A shard job
+ * records two n-bit bitmaps per round (exchange_ms of gp_round_stats). */
+typedef int (*gp_allgather_fn)(void* user, const void* send, int64_t bytes, void* recv);   /* recv: [nranks][bytes] */
+int gp_shard_comm_init(gp_ctx* ctx, const void* unique_id128, int32_t nranks, int32_t rank);
+int gp_shard_host_init(gp_ctx* ctx, gp_allgather_fn fn, void* user, int32_t nranks, int32_t rank);
+/* the communicator's own count and rank (ncclCommCount / ncclCommUserRank), or
+ * those given to gp_shard_host_init; transport_out: 1 = RCCL, 2 = host */
+int gp_shard_info(gp_ctx* ctx, int32_t* nranks_out, int32_t* rank_out, int32_t* transport_out);
+/* after gp_run (uninterrupted since gp_reset) on every rank; finalizes first if
+ * needed.  job[0..*rounds_out) = the job's per-round counters (cap >= rounds);
+ * *ms_out (may be NULL) = device time of the combine on the engine stream. */
+int gp_shard_combine(gp_ctx* ctx, gp_round_stats* job, int32_t cap, int32_t* rounds_out, double* ms_out);
 
 /* Checkpoints (no reference counterpart -- the
  * reference's peers keep no state across restarts).  Taken between rounds:

@@ -1,4 +1,4 @@
-// rccl_standin.cpp -- TEST INFRASTRUCTURE: an in-process stand-in for the ten
+// rccl_standin.cpp -- TEST INFRASTRUCTURE: an in-process stand-in for the twelve
 // RCCL entry points libgossip_hip.so calls (nm -u of the library), so that the
 // vertex partition's real RCCL path -- exchange_rccl in csrc/partition.hip: the
 // count all-gather, the grouped ncclSend / ncclRecv of the boundary entries,
@@ -597,6 +597,18 @@ ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   }
   if (comm->stage) (void)hipFree(comm->stage);
   delete comm;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  if (!comm || !count) return ncclInvalidArgument;
+  *count = comm->w->n;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
+  if (!comm || !rank) return ncclInvalidArgument;
+  *rank = comm->rank;
   return ncclSuccess;
 }
 

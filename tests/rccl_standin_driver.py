@@ -134,6 +134,154 @@ def corrupt(pkg):
     print(f"corrupt ok: ranks=2 status={status[0]} {msgs[0]}", flush=True)
 
 
+class ThreadAllGather:
+    """In-process all-gather of byte strings among P threads (the host
+    transport of a shard job, gp_shard_host_init)."""
+
+    def __init__(self, P):
+        self.P = P
+        self.parts = [None] * P
+        self.bar = threading.Barrier(P, timeout=120)
+
+    def fn(self, k):
+        def all_gather(b):
+            self.parts[k] = b
+            self.bar.wait()
+            out = list(self.parts)
+            self.bar.wait()
+            return out
+        return all_gather
+
+
+def run_shard_job(pkg, g, origin, inject, P, crashes, cfg, transport):
+    """A message-shard job of P ranks as P threads on one GPU: rank k runs the
+    whole overlay for its word-aligned block of the table (dist.message_shard),
+    stops when its own messages quiesce, finalizes and joins gp_shard_combine
+    over the stand-in RCCL (transport "rccl") or the host all-gather ("host").
+    Returns every rank's job record."""
+    m = len(origin)
+    inj = np.zeros(m, np.int32) if inject is None else np.asarray(inject, np.int32)
+    uid = pkg.GossipEngine.comm_unique_id() if transport == "rccl" else None
+    hag = ThreadAllGather(P) if transport == "host" else None
+    engs = []
+    for k in range(P):
+        e = pkg.GossipEngine(0, **cfg)
+        e.load_graph(g)
+        lo, hi = pkg.dist.message_shard(m, P, k)
+        e.set_message_shard(origin, inj, lo, hi)
+        e.reset()
+        engs.append((e, int(inj[lo:hi].max())))
+    by_round = {}
+    for v, r in crashes:
+        by_round.setdefault(r, []).append(v)
+    out = [None] * P
+    errs = []
+
+    def rank(k):
+        try:
+            e, last = engs[k]
+            if transport == "rccl":
+                e.shard_comm_init(uid, P, k)
+            else:
+                e.shard_host_init(hag.fn(k), P, k)
+            info = e.shard_info()
+            assert info == (P, k, 1 if transport == "rccl" else 2), info
+            reports = set()
+            for r in range(254):
+                if r in by_round:
+                    e.crash(by_round[r])
+                st = e.round()
+                rep, nrep = e.reports()
+                assert nrep == len(rep)
+                reports |= set(map(tuple, rep.tolist()))
+                if st["new_bits"] == 0 and r >= last:
+                    break
+            e.finalize()
+            job, ms = e.combine()
+            fwd = None
+            try:
+                fwd = e.job_forwards(m)
+            except pkg.GossipError as x:
+                assert x.status == pkg._lib.GP_ENOTRACK
+            out[k] = dict(job=job, ms=ms, digest=e.job_digest(), cov=e.job_coverage(m), fwd=fwd, reports=reports)
+        except BaseException as exc:
+            errs.append((k, exc))
+
+    ts = [threading.Thread(target=rank, args=(k,)) for k in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e, _ in engs:
+        e.close()
+    if errs:
+        raise RuntimeError(f"rank failures: {[(k, repr(e)) for k, e in errs]}")
+    return out
+
+
+def check_shards(pkg, g, origin, inject, P, crashes, cfg, ref, transport, tag):
+    """The job record every rank holds equals the oracle's whole run: per-round
+    counters (receivers / active as unions), digest, coverage, forwards, and the
+    dead-node reports of the ranks together."""
+    out = run_shard_job(pkg, g, origin, inject, P, crashes, cfg, transport)
+    for o in out:
+        assert len(o["job"]) == ref["rounds"], (tag, len(o["job"]), ref["rounds"])
+        for a, b in zip(o["job"], ref["stats"]):
+            for k in STAT_KEYS:
+                assert a[k] == b[k], (tag, k, a["round"], a[k], b[k])
+        assert np.array_equal(o["digest"], ref["digest"]), tag
+        assert np.array_equal(o["cov"], ref["coverage"]), tag
+        if o["fwd"] is not None:
+            assert np.array_equal(o["fwd"], ref["forwards"]), tag
+        else:
+            assert cfg.get("churn") and not cfg.get("track_msg_forwards"), tag
+    reports = set().union(*(o["reports"] for o in out))
+    assert reports == set(map(tuple, ref["reports"].tolist())), tag
+    return max(o["ms"] for o in out)
+
+
+def shards(pkg):
+    """Message-shard jobs through gp_shard_combine: P = 1-4 on a BA overlay
+    (200 messages, the reference cadence of 4 inject rounds, with and without
+    churn), P = 2, 4, 8 on a Chung-Lu overlay with hubs (4096 messages: rank
+    rows of 32, 16, 8 words), both transports."""
+    cases = 0
+    g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
+    origin = pkg.overlay.random_origins(g.n, 200, seed=8)
+    inject = (np.arange(200) % 4).astype(np.int32)
+    for churn in (False, True):
+        kw = dict(churn=True, p_fail=0.02, churn_seed=3) if churn else {}
+        crashes = [(int(origin[5]), 1), (17, 2)] if churn else []
+        ref = oracle.run(g, origin, inject, crashes=crashes, want_first=True, **kw)
+        for P in (1, 2, 3, 4):
+            for transport in ("rccl", "host"):
+                cfg = dict(track_msg_forwards=int(churn))
+                if churn:
+                    cfg.update(churn=1, p_fail=0.02, churn_seed=3)
+                tag = f"shards ba3001 churn={churn} P={P} {transport}"
+                t0 = time.time()
+                ms = check_shards(pkg, g, origin, inject, P, crashes, cfg, ref, transport, tag)
+                cases += 1
+                print(f"ok  {tag}: combine {ms:.3f} ms, {time.time() - t0:.2f} s", flush=True)
+    rp, col = oracle.chung_lu(50_000, 10, 2.4, 19)
+    g = pkg.CSR(50_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 4096, seed=19)
+    for churn in (False, True):
+        kw = dict(churn=True, p_fail=0.01, churn_seed=6) if churn else {}
+        ref = oracle.run(g, origin, None, nthreads=8, **kw)
+        for P in (2, 4, 8):
+            for transport in (("rccl", "host") if P == 4 else ("rccl",)):
+                cfg = dict(hub_threshold=512)
+                if churn:
+                    cfg.update(churn=1, p_fail=0.01, churn_seed=6)
+                tag = f"shards chung-lu 5e4 x 4096 churn={churn} P={P} {transport}"
+                t0 = time.time()
+                ms = check_shards(pkg, g, origin, None, P, [], cfg, ref, transport, tag)
+                cases += 1
+                print(f"ok  {tag}: combine {ms:.3f} ms, {time.time() - t0:.2f} s", flush=True)
+    print(f"shard cases ok: {cases}", flush=True)
+
+
 def main():
     pkg = _gossip_pkg.load()
     lib_path = pkg._lib.load()._name
@@ -142,6 +290,9 @@ def main():
           flush=True)
     if "--corrupt" in sys.argv:
         corrupt(pkg)
+        return
+    if "--shards" in sys.argv:
+        shards(pkg)
         return
     cases = 0
     # small BA overlay: every P, slice rule, churn setting and mode

@@ -26,7 +26,7 @@ def test_library_exports_every_symbol(pkg):
     raw = ctypes.CDLL(pkg._lib.LIB_PATH)
     for name in declared_symbols():
         assert hasattr(raw, name), name
-    assert lib.gp_abi_version() == pkg._lib.ABI_VERSION == 17
+    assert lib.gp_abi_version() == pkg._lib.ABI_VERSION == 18
 
 
 def test_no_gpu_is_an_error_not_a_fallback(pkg):

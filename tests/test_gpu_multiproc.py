@@ -1,8 +1,8 @@
 """The multi-process launch of bench.py on the GPU box: real engine processes
-(one context each, both on cuda:0 of the one-GPU box) over dist.py's TCP
-control plane, message shards.  The 2-, 3- and 4-rank
-whole-job edge-deliveries must equal the 1-rank run's, and neither process may load
-PyTorch."""
+(one context each, all on cuda:0 of the one-GPU box) over dist.py's TCP
+control plane, message shards.  The 2-, 3- and 4-rank jobs'
+whole-job record (counters, digest, coverage, forwards: gp_shard_combine)
+must equal the 1-rank run's, and no process may load PyTorch."""
 import json
 import os
 import socket
@@ -54,6 +54,13 @@ def test_multi_process_message_shards(world):
     assert many["n_gpus"] == world and f"message-shard x{world}" in many["config"]["parallelism"]
     for k in ("n", "arcs", "messages", "edge_deliveries_per_step", "rounds_per_step"):
         assert many["config"][k] == one["config"][k], k
+    # the job's record, combined inside every step (gp_shard_combine over the
+    # host all-gather: the ranks share the box's one GPU), equals the 1-GPU
+    # run's: per-round receivers / senders as unions over the shards, the
+    # per-vertex digest, per-message coverage and forwards (Peer.py:175-216)
+    assert many["config"]["comm"]["comm_ranks"] == world
+    assert many["config"]["comm"]["transport"].startswith("host")
+    assert many["config"]["job"] == one["config"]["job"]
     w0 = 64 // world   # rank 0's words, rounded up to a power of two
     assert many["config"]["words_per_row"] == 1 << (w0 - 1).bit_length() and one["config"]["words_per_row"] == 64
 

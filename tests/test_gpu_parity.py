@@ -908,8 +908,12 @@ def test_compact_message_lists(pkg, oracle, prefilter, churn):
     g = pkg.CSR(200_000, rp, col, False)
     origin = pkg.overlay.random_origins(g.n, 4096, seed=31)
     kw = dict(churn=True, p_fail=0.01, churn_seed=3) if churn else {}
+    # no hub splits: in early-exit rounds a split hub's chunks stop once one
+    # of them covers the target (hub_done), so how much the chunks scan -- the
+    # work counters compared below, not the rows -- depends on wave timing
+    hub = max(4096, int(np.diff(rp).max()) + 1)
     r = _compare(pkg, oracle, g, origin, first=True, push_ratio=0.0, prefilter_pct=prefilter, arc_mask_permille=0,
-                 compact_rows=1, **kw)
+                 compact_rows=1, hub_threshold=hub, **kw)
     assert any(s["scan"] & 4 for s in r["stats"])
     assert any((s["scan"] & 3) == (3 if prefilter else 0) and s["scan"] & 4 for s in r["stats"])
     r["eng"].close()
@@ -917,7 +921,7 @@ def test_compact_message_lists(pkg, oracle, prefilter, churn):
         return
     # (the same work without records: degree-split rounds off, as record rounds never split)
     with pkg.GossipEngine(0, track_digest=1, push_ratio=0.0, prefilter_pct=prefilter, compact_rows=0,
-                          arc_mask_permille=0, unfiltered_pct=90, flat_max_words=16, hub_threshold=4096,
+                          arc_mask_permille=0, unfiltered_pct=90, flat_max_words=16, hub_threshold=hub,
                           split_deg=0) as eng:
         eng.load_graph(g)
         eng.set_messages(origin)
@@ -1090,3 +1094,94 @@ def test_finalize_paths_agree(pkg, oracle, m, churn, monkeypatch):
     ref = oracle.run(g, origin, **okw)
     assert np.array_equal(cov_c, ref["coverage"]) and np.array_equal(cov_r, ref["coverage"])
     assert np.array_equal(fwd_c, ref["forwards"]) and np.array_equal(fwd_r, ref["forwards"])
+
+
+# (push_ratio, unfiltered_pct, hub_threshold): pull with the activity probe;
+# unfiltered dense rounds; adaptive direction (the last rounds push: their
+# aliased senders are materialized first); hubs split over waves (their chunks
+# probe the done bitmap too)
+ALIAS_MODES = {"pull": (0.0, 0, 1 << 30), "unfiltered": (0.0, 50, 1 << 30), "adaptive": (10.0, 90, 4096),
+               "hubs": (0.0, 90, 256)}
+
+
+@pytest.mark.parametrize("mode", list(ALIAS_MODES))
+def test_aliased_message_lists(pkg, oracle, mode):
+    """W = 64 early-exit rounds with the done bitmap, no liveness, one context
+    (DESIGN.md §3.2): every arc the pull scans probes the done bitmap, and a
+    receiver that completes its component commits SLOT_CMASK instead of a
+    512-B row.  The run equals the oracle's: counters, first receipts,
+    digests, coverage / forwards and every Message-List (gp_read writes the
+    aliased rows it returns).  Reference: each peer's Message-List,
+    Peer.py:175-216."""
+    push_ratio, unfiltered_pct, hub = ALIAS_MODES[mode]
+    rp, col = oracle.chung_lu(120_000, 12, 2.4, 41)
+    g = pkg.CSR(120_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 4096, seed=41)
+    r = _compare(pkg, oracle, g, origin, first=True, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct,
+                 hub_threshold=hub, arc_mask_permille=0, compact_rows=0)
+    st = r["stats"]
+    assert sum(s["aliased"] for s in st) > 0
+    assert any(s["scan"] & 64 for s in st)
+    for s in st:   # aliased receivers write no row
+        if s["scan"] & 64:
+            assert s["rows_written"] + s["aliased"] <= s["receivers"]
+    if mode == "adaptive":
+        k = max(i for i, s in enumerate(st) if s["aliased"])
+        assert any(s["mode"] == 1 for s in st[k + 1:]), "no push round after aliasing"
+    r["eng"].close()
+
+
+def test_aliased_rows_materialize_for_every_reader(pkg, oracle, monkeypatch, tmp_path):
+    """Readers of Message-List rows outside the probing pulls see the rows the
+    aliases stand for: the bit-sliced finalize over every row
+    (GP_FINALIZE_ROWS=1), a checkpoint taken right after the first aliasing
+    round and continued in a fresh context, and a crash injected after it
+    (liveness turns on, the rest of the run keeps no alias)."""
+    rp, col = oracle.chung_lu(60_000, 12, 2.4, 43)
+    g = pkg.CSR(60_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 4096, seed=43)
+    cfg = dict(track_first=1, track_digest=1, push_ratio=0.0, compact_rows=0, arc_mask_permille=0)
+    ref = oracle.run(g, origin, None, want_first=True)
+
+    def finish(eng, stats, ref):
+        while True:
+            s = eng.round()
+            stats.append(s)
+            if s["new_bits"] == 0:
+                break
+        eng.finalize()
+        assert len(stats) == ref["rounds"]
+        for a, b in zip(stats, ref["stats"]):
+            for k in STAT_KEYS:
+                assert a[k] == b[k], (k, a["round"])
+        assert np.array_equal(eng.first(), ref["first"])
+        assert np.array_equal(eng.digest(), ref["digest"])
+        assert np.array_equal(eng.coverage(), ref["coverage"])
+        assert np.array_equal(eng.forwards(), ref["forwards"])
+        assert np.array_equal(eng.seen(), ref["seen"][:, :eng.words])
+
+    # the row-by-row finalize
+    monkeypatch.setenv("GP_FINALIZE_ROWS", "1")
+    with _engine(pkg, g, origin, **cfg) as e:
+        finish(e, [], ref)
+    monkeypatch.delenv("GP_FINALIZE_ROWS")
+    # checkpoint after the first aliasing round, continued elsewhere
+    with _engine(pkg, g, origin, **cfg) as e:
+        stats = []
+        while not stats or not stats[-1]["aliased"]:
+            stats.append(e.round())
+        path = tmp_path / "alias.npy"
+        e.save_checkpoint(path)
+        with _engine(pkg, g, origin, **cfg) as f:
+            f.load_checkpoint(path)
+            finish(f, list(stats), ref)
+        finish(e, stats, ref)
+    # a crash after aliasing: the oracle's run with the same crash
+    with _engine(pkg, g, origin, track_msg_forwards=1, **cfg) as e:
+        stats = []
+        while not stats or not stats[-1]["aliased"]:
+            stats.append(e.round())
+        r0 = len(stats)
+        e.crash([int(origin[0]), 7])
+        ref2 = oracle.run(g, origin, None, crashes=[(int(origin[0]), r0), (7, r0)], want_first=True)
+        finish(e, stats, ref2)

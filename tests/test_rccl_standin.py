@@ -20,7 +20,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NCCL_SYMBOLS = ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclGetErrorString", "ncclGroupStart",
-                "ncclGroupEnd", "ncclAllReduce", "ncclAllGather", "ncclSend", "ncclRecv")
+                "ncclGroupEnd", "ncclAllReduce", "ncclAllGather", "ncclSend", "ncclRecv", "ncclCommCount",
+                "ncclCommUserRank")
 
 
 def _standin_lib(pkg):
@@ -82,3 +83,18 @@ def test_exchange_rccl_corrupt_entry_fails_every_rank(pkg, mode):
     the counters' all-reduce carries the count to every rank."""
     out = _driver(pkg, mode, "--corrupt", extra_env={"GP_STANDIN_CORRUPT": "1:2"}, timeout=280)
     assert "corrupt ok: ranks=2 status=-5" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_shard_job_combine_multi_rank(pkg, mode):
+    """Message-shard jobs of P = 1-4 and 8 ranks through gp_shard_combine
+    (csrc/shard.hip: the XOR reduce-scatter of the digests by ncclSend /
+    ncclRecv + the all-gather of the reduced slices, the OR reduce-scatter of
+    the per-round receiver / sender bitmaps, the all-gather of coverage /
+    forwards and counters), over the stand-in RCCL and over the host
+    all-gather: every rank's job record equals the oracle's whole run,
+    with and without churn (Peer.py:175-216, each peer's whole receive record)."""
+    out = _driver(pkg, mode, "--shards", timeout=580)
+    assert "shard cases ok: 24" in out
