@@ -223,8 +223,10 @@ def cpu_baseline(args, eng, origin, pkg):
     """CPU legs, timed on this box's host cores (reported beside the GPU
     line, never the target):
       port     oracle/gossip_oracle.c (OpenMP) with every thread of the
-               process's affinity set -- `value` -- and again with the
-               OMP_NUM_THREADS share when the environment sets fewer, running ALL
+               process's affinity set, and again with the OMP_NUM_THREADS
+               share when the environment sets fewer (`value`: the faster
+               leg; on the GPU box's EPYC 9575F 256 threads ran 3.4x slower
+               than 16, profiles/r06_bench_c4.json), running ALL
                `messages` (W = 64 words per Message-List row, the GPU's layout)
                to quiescence on a 2^cpu_log2n-vertex overlay of the same
                Chung-Lu recipe and seed: by default the workload itself, on
@@ -265,8 +267,9 @@ def cpu_baseline(args, eng, origin, pkg):
                                f"{', the GPU run overlay' if ncpu == eng.n else ''}), all {len(o)} messages (W = 64), "
                                f"full run{' with churn' if churn else ''} ({ref['rounds']} rounds, {sends} "
                                f"edge-deliveries, {dt:.1f} s, {t} OpenMP threads of {nproc})"})
-    out = {"value": legs[0]["value"], "unit": "GTEPS", "cores": legs[0]["cores"], "kind": "port",
-           "sample": legs[0]["sample"],
+    best = max(legs, key=lambda x: x["value"])   # (the fastest leg: 256 threads ran slower than 16 here)
+    out = {"value": best["value"], "unit": "GTEPS", "cores": best["cores"], "kind": "port",
+           "sample": best["sample"],
            "host": {"nproc": nproc, "affinity": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
                     "cpu_model": model}}
     # leg 2: the per-peer Python harness, single core, BASELINE config 2
@@ -456,8 +459,8 @@ def main():
                                        f"+ all-gather, OR reduce-scatter of the round bitmaps, all-gather of "
                                        f"coverage / forwards / counters)"
                                        if shards else
-                                       f"vertex-partition x{world}" + (" (sparse boundary exchange, ncclSend/Recv)"
-                                                                      if world > 1 else "")),
+                                       (f"vertex-partition x{world} (sparse boundary exchange, ncclSend/Recv)"
+                                        if world > 1 else "one GPU")),
                        "comm": comm,
                        "job": record,
                        "setup_s": round(setup_s, 2), "build_s": round(build_s, 2),

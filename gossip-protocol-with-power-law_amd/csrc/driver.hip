@@ -469,24 +469,30 @@ static int launch_expand(Ctx* c) {
       c->round > c->sate_since)
     c->dnb_now = true;
   // aliased Message-Lists (W = 64, no liveness, one context,
-  // no compact records): in done-neighbour rounds every arc the pull scans
-  // probes the done bitmap (a receiver with any done in-neighbour takes its
-  // target) and receivers that complete commit SLOT_CMASK instead of a
-  // 512-B row.  Once a run holds aliases every later pull is such a round
-  // (held bits only grow, so early exit and the done bitmap stay on), and a
-  // push round first writes its aliased senders' rows (k_unalias)
-  const bool alias_ok = c->words == 64 && !c->liveness_active && !c->local && c->nloc() == c->n_alloc &&
+  // no compact records): in done-neighbour rounds receivers that complete
+  // commit SLOT_CMASK instead of a 512-B row.  Once a run holds aliases every
+  // pull probes the done bitmap for each arc it scans (a receiver with any
+  // done in-neighbour takes its target, so no aliased row slot is gathered);
+  // held bits only grow, so early exit and the done bitmap stay on.  The
+  // first aliasing round reads rows written before any alias and needs no
+  // probe (C4 round 4: 74.6 M arcs whose probe would sit in each pass's
+  // dependent chain).  A push round first writes its aliased senders' rows
+  // (k_unalias)
+#ifndef GP_ALIAS
+#define GP_ALIAS 1
+#endif
+  const bool alias_ok = GP_ALIAS && c->words == 64 && !c->liveness_active && !c->local && c->nloc() == c->n_alloc &&
                         c->cfg.compact_rows == 0 && c->words > c->cfg.flat_max_words;
-  c->dprobe_now = c->dnb_now && alias_ok;
-  c->alias_now = c->dprobe_now;
-  if (c->alias_active) {
-    if (c->mode_push) GP_TRY(unalias(c, true));
-    else if (!c->dprobe_now) GP_TRY(unalias(c, false));   // (a pull that could gather a done sender's row)
-  }
+  c->alias_now = c->dnb_now && alias_ok;
+  c->dprobe_now = c->alias_now && c->alias_active;
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8 * GS))),
                      dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc,
                      c->d_seenpop, c->d_done_at, c->dnb_now ? c->d_dbits : nullptr,
                      c->dnb_now && c->liveness_active ? (const uint8_t*)c->d_state : nullptr);
+  if (c->alias_active) {   // (after k_mkbits: a push round's senders are the activity bitmap's bits)
+    if (c->mode_push) GP_TRY(unalias(c, true));
+    else if (!c->dprobe_now) GP_TRY(unalias(c, false));   // (a pull that could gather a done sender's row)
+  }
   // filtered pull: probe every arc inside the scan, or build the per-arc mask
   // first (pays once the probes are many: senders >= arc_mask_permille of n)
   c->arc_mask_now = !c->mode_push && !c->unfiltered_now && c->cfg.arc_mask_permille > 0 &&

@@ -155,7 +155,8 @@ struct ExpandArgs {
   int32_t dprobe;                      // early exit + dbits (W = 64 pulls): every scanned arc probes the done
                                        //   bitmap first; a done in-neighbour anywhere makes the receiver's
                                        //   new bits its target (done_nb's rule) -- no aliased row is gathered
-  int32_t alias;                       // dprobe rounds: receivers that complete commit SLOT_CMASK, no row
+  int32_t alias;                       // done-neighbour rounds (W = 64, no liveness): receivers that complete
+                                       //   commit SLOT_CMASK, no row (every later pull is a dprobe round)
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
   int32_t near_done;                   // early-exit round with most messages held: fewer rows in flight
   const u64* __restrict__ alive;       // [W] messages some sender forwards this round (or null)

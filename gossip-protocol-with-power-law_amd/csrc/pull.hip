@@ -1148,17 +1148,20 @@ __global__ __launch_bounds__(BLOCK) void k_arcmask(const int32_t* __restrict__ g
 // One wave per 64-vertex bitmap word; fully active words cost two loads.
 // (Only without liveness: a crashed vertex may hold bits it never sent.)
 // Materialize aliased Message-Lists (SLOT_CMASK): write the
-// component row of every aliased vertex (with fpop: of this round's senders
-// only, before a push round reads them) into S[cur] and point sp there.  One
-// wave per 64 vertices, a row per aliased vertex in one coalesced store.
+// component row of every aliased vertex (with abits: of this round's senders
+// only, before a push round reads them -- the 2 MB activity bitmap first, the
+// slot bytes of its set bits only) into S[cur] and point sp there.  One wave
+// per 64 vertices, a row per aliased vertex in one coalesced store.
 __global__ __launch_bounds__(BLOCK) void k_unalias(uint8_t* __restrict__ sp, uint8_t* __restrict__ ws,
-                                                   const uint32_t* __restrict__ fpop, const int32_t* __restrict__ midx,
+                                                   const u64* __restrict__ abits, const int32_t* __restrict__ midx,
                                                    const u64* __restrict__ cmask, u64* __restrict__ rows,
                                                    int32_t cur, int64_t n, int32_t W) {
   const int lane = threadIdx.x & 63;
   for (int64_t w = (int64_t)blockIdx.x * WAVES + (threadIdx.x >> 6); w * 64 < n; w += (int64_t)gridDim.x * WAVES) {
     const int64_t v = w * 64 + lane;
-    const bool al = v < n && sp[v] == SLOT_CMASK && (!fpop || fpop[v] != 0u);
+    const u64 sel = abits ? abits[w] : ~0ull;
+    if (sel == 0ull) continue;
+    const bool al = v < n && ((sel >> lane) & 1ull) && sp[v] == SLOT_CMASK;
     u64 todo = __ballot(al);
     if (al) {
       sp[v] = (uint8_t)cur;
@@ -1177,7 +1180,7 @@ __global__ __launch_bounds__(BLOCK) void k_unalias(uint8_t* __restrict__ sp, uin
 int unalias(Ctx* c, bool senders_only) {
   if (!c->alias_active) return 0;
   hipLaunchKernelGGL(k_unalias, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8 * GS)),
-                     dim3(BLOCK), 0, c->stream, c->d_sp, c->d_ws, senders_only ? c->d_fpop[c->cur] : nullptr,
+                     dim3(BLOCK), 0, c->stream, c->d_sp, c->d_ws, senders_only ? c->d_abits : nullptr,
                      c->d_midx, c->d_cmask, c->d_slot[c->cur], c->cur, c->n_alloc, c->words);
   GP_HIP(hipGetLastError());
   if (!senders_only) c->alias_active = false;

@@ -246,7 +246,8 @@ void pack_stats(const gp_round_stats& s, u64* f) {
 }
 
 // header words all-gathered first: every rank validates every rank's shape
-enum { H_N, H_NNZ, H_M, H_WORDS, H_WBASE, H_ROUNDS, H_DIGEST, H_FWD, H_CHURN, H_SEED, H_PFAIL, H_DIRECTED, NH = 16 };
+enum { H_N, H_NNZ, H_M, H_WORDS, H_WBASE, H_ROUNDS, H_DIGEST, H_FWD, H_CHURN, H_SEED, H_PFAIL, H_DIRECTED, H_OK,
+       NH = 16 };
 
 int ensure_scratch(Ctx* c, size_t words) {
   if (c->jscr_words >= words) return 0;
@@ -262,10 +263,15 @@ int combine(Ctx* c, gp_round_stats* job, int32_t cap, int32_t* rounds_out, doubl
   hipStream_t s = c->stream;
   Xport x{c, P, me};
   const int32_t own = c->round;
+  // a rank that cannot take part still joins the header all-gather, so that
+  // every rank returns the same status instead of its peers waiting in a
+  // collective it never enters
+  std::string why;
   if (own < 1 || (int32_t)c->run_stats.size() != own || c->hist_rounds != own)
-    return set_error(GP_ESTATE, "gp_shard_combine needs a run of gp_round / gp_run since gp_reset on this "
-                                "context (a run restored from a checkpoint has no per-round history)");
-  if (c->fin_round != c->round) GP_TRY(gp_finalize_messages(static_cast<gp_ctx*>(c)));
+    why = "gp_shard_combine needs a run of gp_round / gp_run since gp_reset on this context (a run restored "
+          "from a checkpoint has no per-round history)";
+  else if (c->fin_round != c->round && gp_finalize_messages(static_cast<gp_ctx*>(c)) != 0)
+    why = std::string("finalize: ") + gp_last_error();
   GP_HIP(hipEventRecord(c->ev[0], s));
 
   // 1. headers: shapes, the shards' message blocks, the rounds each ran
@@ -277,6 +283,7 @@ int combine(Ctx* c, gp_round_stats* job, int32_t cap, int32_t* rounds_out, doubl
   hdr[H_FWD] = (!c->msg_forwards_valid && c->liveness_active) ? 0 : 1;
   hdr[H_CHURN] = (u64)c->cfg.churn; hdr[H_SEED] = c->cfg.churn_seed; hdr[H_PFAIL] = dbits(c->cfg.p_fail);
   hdr[H_DIRECTED] = (u64)c->directed;
+  hdr[H_OK] = why.empty() ? 1 : 0;
   GP_TRY(copy_sync(c, c->d_jscr, hdr.data(), NH * 8, hipMemcpyHostToDevice));
   GP_TRY(x.allgather(c->d_jscr, c->d_jscr + NH, NH));
   GP_TRY(copy_sync(c, all.data(), c->d_jscr + NH, all.size() * 8, hipMemcpyDeviceToHost));
@@ -285,6 +292,9 @@ int combine(Ctx* c, gp_round_stats* job, int32_t cap, int32_t* rounds_out, doubl
   std::vector<int> order((size_t)P);
   int32_t R = 0, wmax = 0;
   int64_t mt = 0;
+  if (!why.empty()) return set_error(GP_ESTATE, why);
+  for (int q = 0; q < P; ++q)
+    if (!H(q, H_OK)) return set_error(GP_ESTATE, "gp_shard_combine: rank " + std::to_string(q) + " has no run to combine");
   for (int q = 0; q < P; ++q) {
     for (int k : {H_N, H_NNZ, H_DIGEST, H_CHURN, H_SEED, H_PFAIL, H_DIRECTED})
       if (H(q, k) != H(0, k))

@@ -279,6 +279,41 @@ def shards(pkg):
                 ms = check_shards(pkg, g, origin, None, P, [], cfg, ref, transport, tag)
                 cases += 1
                 print(f"ok  {tag}: combine {ms:.3f} ms, {time.time() - t0:.2f} s", flush=True)
+    # a rank with no run to combine: every rank fails the combine with the
+    # same status (it still joins the header all-gather), none waits forever
+    g = pkg.overlay.barabasi_albert(3001, 2, seed=8)
+    origin = pkg.overlay.random_origins(g.n, 200, seed=8)
+    uid = pkg.GossipEngine.comm_unique_id()
+    engs = []
+    for k in range(2):
+        e = pkg.GossipEngine(0)
+        e.load_graph(g)
+        lo, hi = pkg.dist.message_shard(200, 2, k)
+        e.set_message_shard(origin, None, lo, hi)
+        e.reset()
+        engs.append(e)
+    status = [None, None]
+
+    def fail_rank(k):
+        e = engs[k]
+        e.shard_comm_init(uid, 2, k)
+        if k == 0:
+            e.run()
+            e.finalize()
+        try:
+            e.combine()
+        except pkg.GossipError as x:
+            status[k] = x.status
+
+    ts = [threading.Thread(target=fail_rank, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts), "a rank hung in the combine"
+    for e in engs:
+        e.close()
+    assert status == [pkg._lib.GP_ESTATE] * 2, status
     print(f"shard cases ok: {cases}", flush=True)
 
 

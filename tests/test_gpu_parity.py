@@ -928,9 +928,16 @@ def test_compact_message_lists(pkg, oracle, prefilter, churn):
         eng.reset()
         stats = eng.run()
         assert not any(s["scan"] & 4 for s in stats)
+        # (without records the late rounds alias complete receivers instead of
+        # writing their rows, and once aliases exist every scanned arc probes
+        # the done bitmap, which can stop a scan before the early exit would)
         for a, b in zip(stats, r["stats"]):
-            for k in STAT_KEYS + ("rows_gathered", "arcs_scanned", "rows_written"):
+            for k in STAT_KEYS:
                 assert a[k] == b[k], k
+            assert a["rows_written"] + a["aliased"] == b["rows_written"] and b["aliased"] == 0
+            if not a["scan"] & 64:
+                for k in ("rows_gathered", "arcs_scanned"):
+                    assert a[k] == b[k], k
         assert np.array_equal(eng.digest(), r["ref"]["digest"])
 
 
