@@ -94,6 +94,22 @@ __global__ __launch_bounds__(HBLOCK) void k_hub_final(ExpandArgs a) {
           if (a.hub_pnz[p]) acc |= load_piece<W>(a.hub_partial, p, lw);
         if (a.prehi) acc |= load_piece<W>(a.acc, v, lw);   // degree-split round: the push half's OR (k_acc_clear zeroes it)
       }
+      // alive early-exit rounds with no injection left (liveness, DESIGN.md
+      // §3.5): a hub whose chunks covered every alive message of its
+      // component it lacked is sated, as k_expand marks its receivers.  Hubs
+      // are the first in-neighbours of most gather orders, so their marks are
+      // what the next round's done-neighbour probe finds
+#ifndef GP_HUB_SATE
+#define GP_HUB_SATE 1
+#endif
+      if (GP_HUB_SATE && a.sate && a.early_exit && a.alive) {
+        u64x2 rem = {0, 0};
+        if (g == 0) {
+          const u64x2 sv = load_seen<W>(a, v, a.sp[v], lw);
+          rem = load_piece<W>(a.cmask, a.midx[v], lw) & load_piece<W>(a.alive, 0, lw) & ~sv & ~acc;
+        }
+        if (!__any((rem.x | rem.y) != 0ull) && lane == 0) a.state[v] |= ST_SATED;
+      }
       finish_row<W>(a, v, i, acc, lane, g, lw, st, s_w[wib], false, a.sp[v]);
     }
   }
