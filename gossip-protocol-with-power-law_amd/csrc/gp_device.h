@@ -384,7 +384,10 @@ enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PR
                 SCAN_ALIVE = 8 /* flag: early-exit targets narrowed to the alive messages (k_expand);
                                   a variant of its own: +2-3 VGPRs cost a wave per SIMD */,
                 SCAN_LINES = 32 /* flag (W = 64, filtered): the probe reads the sender's line mask
-                                   (k_mklm) and the gather loads only its nonzero 128-B lines */ };
+                                   (k_mklm) and the gather loads only its nonzero 128-B lines */,
+                SCAN_DPROBE = 64 /* flag (k_expand, W = 64, filtered / unfiltered): every scanned arc
+                                    probes the done bitmap (a.dprobe rounds, aliased Message-Lists);
+                                    a variant of its own: +4 VGPRs cost the unfiltered pull a wave */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
@@ -617,8 +620,10 @@ __device__ __forceinline__ u64x2 early_exit_target(const ExpandArgs& a, int v, L
 }
 
 // per-receiver scan of arcs [b, e): 64 arcs per pass -- column ids, activity
-// probes, staging, gather
-template <int W, int MODE, class LDS>
+// probes, staging, gather.  DP: the variant can run in a done-probe round
+// (a.dprobe; W = 64 filtered / unfiltered pulls without liveness): compiled
+// out elsewhere, so the other variants keep their registers
+template <int W, int MODE, bool DP, class LDS>
 __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int64_t e, LDS& L, int lane,
                                             int g, int lw, u64x2& acc, WaveStats& st, bool ee, u64x2 want,
                                             int32_t col0 = INT32_MIN) {
@@ -678,13 +683,13 @@ __device__ __forceinline__ void gather_scan(const ExpandArgs& a, int64_t b, int6
       u64 dw = 0;
       if (lane < n) {
         u = (col0 != INT32_MIN && j0 == b) ? col0 : a.gcol[j0 + lane];
-        if (a.dprobe) dw = a.dbits[u >> 6];   // (beside the activity probe: one round trip)
+        if (DP && a.dprobe) dw = a.dbits[u >> 6];   // (beside the activity probe: one round trip)
         ent = probe<MODE>(a, u);
       }
       // a done in-neighbour in this pass: the receiver's new bits are its
       // whole target (done_nb's rule, any arc), and none of the pass's rows
       // is gathered -- an aliased sender's row slot holds no Message-List
-      if (a.dprobe && __any(u >= 0 && ((dw >> (u & 63)) & 1ull))) {
+      if (DP && a.dprobe && __any(u >= 0 && ((dw >> (u & 63)) & 1ull))) {
         acc = want;
         break;
       }

@@ -46,7 +46,8 @@ __global__ __launch_bounds__(HBLOCK) void k_hub_partial(ExpandArgs a) {
           if (lane == 0) f = __hip_atomic_load(a.hub_done + h.hub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((uint32_t)__builtin_amdgcn_readfirstlane((int)f) == a.hub_epoch) break;
         }
-        gather_scan<W, MODE>(a, s0, min(hend, s0 + SUB), s_w[wib], lane, g, lw, acc, st, ee, want);
+        gather_scan<W, MODE, W == 64 && (MODE == SCAN_FILTERED || MODE == SCAN_UNFILTERED)>(
+            a, s0, min(hend, s0 + SUB), s_w[wib], lane, g, lw, acc, st, ee, want);
         if (ee) {
           u64x2 t = acc;
           reduce_slots<W>(t);

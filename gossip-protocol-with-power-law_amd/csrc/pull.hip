@@ -166,7 +166,7 @@ __device__ __forceinline__ bool done_nb(const ExpandArgs& a, int64_t b, int64_t 
 // Receivers with a done in-neighbour two at a time, one per half-wave (W =
 // 64): nothing to gather, so each pair is one round trip (its seen rows and
 // the component rows, the latter L2-resident) and the commit
-template <int W, bool ALIVE, class LDS>
+template <int W, bool ALIVE, bool ALIAS, class LDS>
 __device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
                                           WaveStats& st) {
   static_assert(W == 64, "half-wave rows");
@@ -193,7 +193,7 @@ __device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
     const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
     st.add(S_SEEN_READ, (u64)((sA != SLOT_NONE ? 1 : 0) + (kB >= 0 && sB != SLOT_NONE ? 1 : 0)));
-    pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, cm, sv, st, !ALIVE && a.alias != 0);
+    pair_finish<W>(a, L, h, lw, on, ks, kB, i, v, cm, sv, st, ALIAS && a.alias != 0);
   }
 }
 
@@ -213,7 +213,12 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
   const int g = lane / LPR, lw = lane % LPR;
   auto& L = s_w[wib];
   constexpr bool ALIVE = (MODE & SCAN_ALIVE) != 0;
-  constexpr int SCAN = MODE & ~SCAN_ALIVE;
+  constexpr bool DPROBE = (MODE & SCAN_DPROBE) != 0;
+  constexpr int SCAN = MODE & ~(SCAN_ALIVE | SCAN_DPROBE);
+  // the variants done-neighbour rounds without liveness launch: their complete
+  // receivers may alias (a.alias) and their scans probe the done bitmap
+  // (a.dprobe); the other variants compile neither
+  constexpr bool ALIASABLE = W == 64 && !ALIVE && (SCAN == SCAN_FILTERED || SCAN == SCAN_UNFILTERED);
   WaveStats st;
   ws_zero<EWAVES>(st);
   const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * 64;
@@ -381,7 +386,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
     if constexpr (W == 64) {
       if (mdn) {   // done in-neighbours: two receivers at a time, the rest below
         const u64 md = m & mdn;
-        dnb_pairs<W, ALIVE>(a, L, md, base, slot_of, st);
+        dnb_pairs<W, ALIVE, ALIASABLE>(a, L, md, base, slot_of, st);
         if constexpr (ALIVE) {   // they now hold every alive message of their component: sated too
           if (a.sate) sat |= md;
         }
@@ -429,7 +434,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
         if (np != 0xFFu) {
           gather_rows<W>(a, L.pre[k], (int)np, g, lw, acc, st, ee, want);   // full rows
         } else {
-          gather_scan<W, SCAN>(a, vb, vb + L.len[k], L, lane, g, lw, acc, st, ee, want, col0);
+          gather_scan<W, SCAN, false>(a, vb, vb + L.len[k], L, lane, g, lw, acc, st, ee, want, col0);
           if ((tw >> k) & 1ull) {   // degree-split: the accumulator row (not staged: a scanned receiver)
             if (g == 0) acc |= load_piece<W>(a.acc, v, lw);
             st.add(S_GATHERED, 1);
@@ -437,7 +442,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
           }
         }
       } else {
-        gather_scan<W, SCAN>(a, vb, ve, L, lane, g, lw, acc, st, ee, want, col0);
+        gather_scan<W, SCAN, DPROBE>(a, vb, ve, L, lane, g, lw, acc, st, ee, want, col0);
       }
       reduce_slots<W>(acc);
       if constexpr (ALIVE) {   // the round's gather covered every alive message v lacked: sated
@@ -459,7 +464,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
       // alias rounds: a receiver whose gather covered its whole target now
       // holds its component's row (no liveness: want = cm & ~seen)
       bool full = false;
-      if (!ALIVE && a.alias && ee) {
+      if (ALIASABLE && a.alias && ee) {
         const u64x2 rem = want & ~acc;
         full = !__any((rem.x | rem.y) != 0ull);
       }
@@ -1304,6 +1309,13 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     if (alive_ee) {
       if constexpr (W >= 32)
         hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE>), grid, dim3(EBLOCK), 0, c->stream, a);
+    } else if (W == 64 && a.dprobe) {   // (done-probe rounds: filtered or unfiltered, launch_expand)
+      if constexpr (W == 64) {
+        if (mode == SCAN_UNFILTERED)
+          hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_DPROBE>), grid, dim3(EBLOCK), 0, c->stream, a);
+        else
+          hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_DPROBE>), grid, dim3(EBLOCK), 0, c->stream, a);
+      }
     } else if (mode == SCAN_UNFILTERED) {
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(EBLOCK), 0, c->stream, a);
     }
