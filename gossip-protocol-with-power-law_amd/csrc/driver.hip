@@ -71,15 +71,25 @@ __global__ void k_stats_reduce(u64* __restrict__ partial, u64* __restrict__ stat
 // With liveness (sated: the state bytes) the done bitmap is bit v = v is up and
 // sated: it holds every alive message of its component, and
 // the alive sets only shrink once no injection is left.
+// With deg_live (receiver-list rounds, DESIGN.md §3.5: the pull's waves visit
+// only the listed receivers) also every sender's accounting: sends =
+// fpop * deg_live and the active count, into the partial stat slots.
 __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ fpop, u64* __restrict__ abits,
                                                   int64_t n, const uint32_t* __restrict__ seenpop,
                                                   const uint32_t* __restrict__ done_at, u64* __restrict__ dbits,
-                                                  const uint8_t* __restrict__ sated) {
+                                                  const uint8_t* __restrict__ sated,
+                                                  const int32_t* __restrict__ deg_live, u64* __restrict__ partial) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * BLOCK;
+  u64 sends = 0, active = 0;
   for (int64_t v0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63); v0 < n; v0 += stride) {
     const int64_t v = v0 + lane;
-    const u64 m = __ballot(v < n && fpop[v] != 0u);
+    const uint32_t fp = v < n ? fpop[v] : 0u;
+    const u64 m = __ballot(fp != 0u);
+    if (deg_live && fp) {
+      sends += (u64)fp * (u64)(uint32_t)max(deg_live[v], 0);
+      ++active;
+    }
     if (lane == 0) abits[v0 >> 6] = m;
     if (dbits) {
       bool d = false;
@@ -93,6 +103,15 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
       }
       const u64 dm = __ballot(d);
       if (lane == 0) dbits[v0 >> 6] = dm;
+    }
+  }
+  if (deg_live) {
+    sends = wave_sum_u64(sends);
+    active = wave_sum_u64(active);
+    if (lane == 0) {
+      const size_t p = blockIdx.x % NPART;
+      if (sends) atomicAdd(&partial[(size_t)S_SENDS * NPART + p], sends);
+      if (active) atomicAdd(&partial[(size_t)S_ACTIVE * NPART + p], active);
     }
   }
 }
@@ -334,6 +353,9 @@ static void fill_expand(Ctx* c, ExpandArgs& a) {
   a.early_exit = c->early_exit_now ? 1 : 0;
   a.dprobe = c->dprobe_now ? 1 : 0;
   a.alias = c->alias_now ? 1 : 0;
+  a.ulist = c->ulist_read_now ? c->d_ulist[c->ul_cur] : nullptr;
+  a.ulist_n = c->ulist_read_now ? c->ulist_n : 0;
+  a.ulist_next = c->ulist_emit_now ? c->d_ulist[c->ul_cur ^ 1] : nullptr;
   a.fpop_next = c->d_fpop[c->cur ^ 1];
   a.seenpop = c->d_seenpop;
   a.first = c->cfg.track_first ? c->d_first : nullptr;
@@ -485,10 +507,25 @@ static int launch_expand(Ctx* c) {
                         c->cfg.compact_rows == 0 && c->words > c->cfg.flat_max_words;
   c->alias_now = c->dnb_now && alias_ok;
   c->dprobe_now = c->alias_now && c->alias_active;
+  // receiver lists (W = 64 early-exit pulls, one context):
+  // once most messages are held, each pull appends the receivers that stay
+  // neither done nor sated; a pull whose list is under a third of the
+  // vertices launches waves for those alone, k_mkbits does every sender's
+  // accounting and the receivers' fpop_next starts zeroed (C5 round 6: 1.26 M
+  // receivers of 64 M vertices)
+#ifndef GP_ULIST
+#define GP_ULIST 1
+#endif
+  const bool list_ok = GP_ULIST && !c->mode_push && !c->local && c->nloc() == c->n_alloc && c->words == 64 &&
+                       c->words > c->cfg.flat_max_words && c->cfg.compact_rows == 0 && c->early_exit_now;
+  c->ulist_read_now = list_ok && c->ulist_valid && c->ulist_n * 3 < c->n_alloc;
+  if (c->ulist_read_now)
+    GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1], 0, (size_t)c->nloc() * 4, c->stream));
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8 * GS))),
                      dim3(BLOCK), 0, c->stream, c->d_fpop[c->cur], c->d_abits, c->n_alloc,
                      c->d_seenpop, c->d_done_at, c->dnb_now ? c->d_dbits : nullptr,
-                     c->dnb_now && c->liveness_active ? (const uint8_t*)c->d_state : nullptr);
+                     c->dnb_now && c->liveness_active ? (const uint8_t*)c->d_state : nullptr,
+                     c->ulist_read_now ? (const int32_t*)c->d_deg_live : nullptr, c->d_stats + 64);
   if (c->alias_active) {   // (after k_mkbits: a push round's senders are the activity bitmap's bits)
     if (c->mode_push) GP_TRY(unalias(c, true));
     else if (!c->dprobe_now) GP_TRY(unalias(c, false));   // (a pull that could gather a done sender's row)
@@ -556,9 +593,19 @@ static int launch_expand(Ctx* c) {
     c->split_now = row > 0 && row + c->nloc() <= (int64_t)INT32_MAX;
     c->acc_row = (int32_t)row;
   }
-  if (c->dprobe_now) {   // the scan modes whose gathers probe the done bitmap: filtered and unfiltered
+  if (c->dprobe_now || c->ulist_read_now) {   // the scan modes of these variants: filtered and unfiltered
     c->arc_mask_now = c->prefilter_now = c->split_now = false;
     c->cml_read_now = c->cml_write_now = c->lines_now = c->lm_write_now = false;
+  }
+  c->ulist_emit_now = list_ok && (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m && !c->arc_mask_now &&
+                      !c->prefilter_now && !c->split_now && !c->cml_read_now && !c->cml_write_now && !c->lines_now;
+  if (c->ulist_emit_now && !c->d_ulist[0]) {
+    if (dalloc(&c->d_ulist[0], (size_t)c->n_alloc) != 0 || dalloc(&c->d_ulist[1], (size_t)c->n_alloc) != 0) {
+      dfree(&c->d_ulist[0]);   // (out of memory: no lists)
+      dfree(&c->d_ulist[1]);
+      c->ulist_emit_now = false;
+      (void)hipGetLastError();
+    }
   }
   if (narrow_split && !c->split_now)   // (the conditions above mirror these: a pull was promised a split)
     return set_error(GP_ESTATE, "internal: narrow-row split round not eligible");
@@ -741,7 +788,7 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
     out->scan = c->mode_push ? 0 : (c->unfiltered_now ? 2 : c->arc_mask_now ? 1 : c->prefilter_now ? 3 : 0) |
                                        (c->cml_read_now ? 4 : 0) | (c->lines_ran ? 8 : 0) |
                                        (c->lines_from_commits ? 16 : 0) | (c->split_now ? 32 : 0) |
-                                       (c->dprobe_now ? 64 : 0);
+                                       (c->dprobe_now ? 64 : 0) | (c->ulist_read_now ? 128 : 0);
     out->kernel_ms = 0.0;
     if (!c->mode_push && c->nloc() > 0) {
       float kms = 0.f;
@@ -772,6 +819,12 @@ static int round_collect(Ctx* c, gp_round_stats* out) {
   c->cml_written_prev = c->cml_write_now;
   c->lm_written_prev = c->lm_write_now;
   if (h[S_ALIASED]) c->alias_active = true;
+  c->ulist_valid = c->ulist_emit_now;   // (a round that appends no list ends the last one)
+  if (c->ulist_emit_now) {
+    c->ulist_n = (int64_t)h[S_ULIST];
+    c->ul_cur ^= 1;
+  }
+  c->ulist_emit_now = c->ulist_read_now = false;
   c->cur ^= 1;
   c->round = r + 1;
   return 0;

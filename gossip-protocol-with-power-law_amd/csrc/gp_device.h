@@ -157,6 +157,10 @@ struct ExpandArgs {
                                        //   new bits its target (done_nb's rule) -- no aliased row is gathered
   int32_t alias;                       // done-neighbour rounds (W = 64, no liveness): receivers that complete
                                        //   commit SLOT_CMASK, no row (every later pull is a dprobe round)
+  const int32_t* __restrict__ ulist;   // SCAN_LIST rounds: the vertices that could still receive
+  int64_t ulist_n;
+  int32_t* __restrict__ ulist_next;    // (or null) the same after this round: each wave appends its
+                                       //   receivers that are still neither done nor sated (late rounds)
   int32_t unfiltered;                  // read every in-neighbour row (k_fixup_rows ran)
   int32_t near_done;                   // early-exit round with most messages held: fewer rows in flight
   const u64* __restrict__ alive;       // [W] messages some sender forwards this round (or null)
@@ -268,9 +272,9 @@ constexpr int PRE_MAX_DEG = 16;  // in-degree up to which the lane phase probes
 #define GP_WAVE_PRE_MAX 64
 #endif
 constexpr int WAVE_PRE_N = 4;   // (2 and 8 measured equal)
-template <bool PRE, bool CML>
+template <bool PRE, bool CML, bool LIST = false>
 struct WaveLdsT {
-  static constexpr bool kPre = PRE, kCml = CML;
+  static constexpr bool kPre = PRE, kCml = CML, kList = LIST;
   u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
   int32_t idx[64];      // active neighbours of one pass
   uint32_t tot[64];     // k_expand: new bits of the wave's vertex k (committed after the loop)
@@ -285,9 +289,11 @@ struct WaveLdsT {
   uint8_t np[PRE ? 64 : 1];       // SCAN_PRE: how many (0xFF: not prefiltered, scan as usual)
   uint32_t len[PRE ? 64 : 1];     // SCAN_PRE: in-arcs vertex k scans (its prefix in degree-split rounds)
   u64 alive[64];                  // OR of the new rows this wave wrote (alive_next)
+  int32_t vid[LIST ? 64 : 1];     // SCAN_LIST: vertex of lane k (the list is not consecutive ids)
+  int64_t re[LIST ? 64 : 1];      // SCAN_LIST: end of vertex k's in-list
 };
 using WaveLds = WaveLdsT<false, false>;
-#define LDS_OF(MODE) WaveLdsT<((MODE) & 3) == SCAN_PRE, ((MODE) & SCAN_CML) != 0>
+#define LDS_OF(MODE) WaveLdsT<((MODE) & 3) == SCAN_PRE, ((MODE) & SCAN_CML) != 0, ((MODE) & SCAN_LIST) != 0>
 
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -387,7 +393,10 @@ enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PR
                                    (k_mklm) and the gather loads only its nonzero 128-B lines */,
                 SCAN_DPROBE = 64 /* flag (k_expand, W = 64, filtered / unfiltered): every scanned arc
                                     probes the done bitmap (a.dprobe rounds, aliased Message-Lists);
-                                    a variant of its own: +4 VGPRs cost the unfiltered pull a wave */ };
+                                    a variant of its own: +4 VGPRs cost the unfiltered pull a wave */,
+                SCAN_LIST = 128 /* flag (k_expand, W >= 32, filtered / unfiltered): the waves take
+                                   their receivers from a.ulist, the vertices that could still
+                                   receive (late rounds), not 64 consecutive ids */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
@@ -849,7 +858,7 @@ __device__ __forceinline__ void finish_row(const ExpandArgs& a, int v, int64_t i
 }
 
 // k_expand's commit of the deferred per-vertex words: lane k holds vertex
-// base + k (need: it was scanned)
+// li = base + k, or in SCAN_LIST rounds the list's vertex (need: it was scanned)
 template <class LDS>
 __device__ __forceinline__ void commit_vertices(const ExpandArgs& a, LDS& L, int64_t li, bool need,
                                                 WaveStats& st) {

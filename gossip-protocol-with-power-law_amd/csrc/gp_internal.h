@@ -31,7 +31,8 @@ enum StatSlot {
   // boundary entries the unpack found inconsistent with the exchange plan
   // (partition.hip k_rx_unpack); all-reduced with the counters, fails the round
   S_XERR = NST + 1,
-  S_REPORT_CURSOR = 26, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR, S_DET_BIG
+  S_REPORT_CURSOR = 26, S_CAND, S_ACTIVE_CURSOR, S_BIG_CURSOR, S_TOUCH_CURSOR, S_DET_BIG,
+  S_ULIST   // entries of the next round's receiver list (k_expand survivors)
 };
 static_assert(S_XERR < S_REPORT_CURSOR, "S_XERR must be inside the all-reduced counter slots");
 
@@ -179,6 +180,14 @@ struct Ctx {
   // alias_now: its complete receivers alias; alias_active: the run holds
   // aliases (readers of rows outside such pulls materialize them, k_unalias)
   bool dprobe_now = false, alias_now = false, alias_active = false;
+  // receiver lists: late early-exit pulls append the
+  // receivers that are still neither done nor sated to d_ulist[ul_cur ^ 1];
+  // the next pull, when the list is short, launches waves for those alone
+  // (SCAN_LIST) and leaves the senders' accounting to k_mkbits
+  int32_t* d_ulist[2] = {nullptr, nullptr};
+  int ul_cur = 0;
+  bool ulist_valid = false, ulist_emit_now = false, ulist_read_now = false;
+  int64_t ulist_n = 0;
   int32_t acc_row = 0;      // its accumulator rows addressed as rows of the round's slot buffer
   // [nnz/64 + 2] per-arc activity mask of filtered pull rounds (gcol order): 33.5 MB at C4
   u64* d_amask = nullptr;

@@ -181,8 +181,12 @@ __device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
     }
     const bool on = h == 0 || kB >= 0;
     const int ks = (h && kB >= 0) ? kB : kA;
-    const int64_t i = base + ks;
-    const int v = (int)(a.vbegin + i);
+    int64_t i = base + ks;
+    int v = (int)(a.vbegin + i);
+    if constexpr (LDS::kList) {   // (list rounds: lane k's vertex)
+      v = L.vid[ks];
+      i = v - a.vbegin;
+    }
     const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
     u64x2 sv = {0, 0}, cm = {0, 0};
     if (on) {
@@ -214,7 +218,10 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
   auto& L = s_w[wib];
   constexpr bool ALIVE = (MODE & SCAN_ALIVE) != 0;
   constexpr bool DPROBE = (MODE & SCAN_DPROBE) != 0;
-  constexpr int SCAN = MODE & ~(SCAN_ALIVE | SCAN_DPROBE);
+  constexpr bool LIST = (MODE & SCAN_LIST) != 0;
+  constexpr int SCAN = MODE & ~(SCAN_ALIVE | SCAN_DPROBE | SCAN_LIST);
+  // the variants that can append this round's survivors to the next list
+  constexpr bool EMIT = W == 64 && (SCAN == SCAN_FILTERED || SCAN == SCAN_UNFILTERED);
   // the variants done-neighbour rounds without liveness launch: their complete
   // receivers may alias (a.alias) and their scans probe the done bitmap
   // (a.dprobe); the other variants compile neither
@@ -222,8 +229,13 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
   WaveStats st;
   ws_zero<EWAVES>(st);
   const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * 64;
-  if (base < a.nloc) {
+  if (base < (LIST ? a.ulist_n : a.nloc)) {
     const int64_t li = base + lane;
+    // lane's vertex (local index): base + lane, or the list's entry (list
+    // rounds: every sender's accounting is k_mkbits', every non-receiver's
+    // fpop_next was zeroed before the launch)
+    const bool valid = LIST ? li < a.ulist_n : li < a.nloc;
+    const int64_t vi = LIST ? (valid ? (int64_t)a.ulist[li] : 0) : li;
     bool need = false, act = false, dnb = false;
     // degree-split rounds: receivers the push half touched (bit k = vertex
     // base + k; one context: local = global ids).  A touched receiver's
@@ -239,16 +251,23 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
     u64 sends = 0;
     uint32_t slot_of = SLOT_NONE;
     uint32_t pre_arcs = 0;   // SCAN_PRE: arcs the lane phase scanned
-    if (li < a.nloc) {
-      const int v = (int)(a.vbegin + li);
-      const uint32_t fp = a.fpop[v];
-      act = fp != 0u;
-      if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
+    if (valid) {
+      const int v = (int)(a.vbegin + vi);
+      if constexpr (!LIST) {
+        const uint32_t fp = a.fpop[v];
+        act = fp != 0u;
+        if (act) sends = (u64)fp * (u64)(uint32_t)max(a.deg_live[v], 0);
+      }
       const int64_t b = a.row_ptr[v], e = a.row_ptr[v + 1];
       L.rp[lane] = b;
-      if (lane == 63 || li + 1 == a.nloc) L.rp[lane + 1] = e;
+      if constexpr (LIST) {
+        L.re[lane] = e;
+        L.vid[lane] = v;
+      } else {
+        if (lane == 63 || li + 1 == a.nloc) L.rp[lane + 1] = e;
+      }
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
-      need = !(a.state[v] & (ST_DOWN | ST_SATED)) && a.seenpop[li] < a.done_at[v] && !hub && e > b;
+      need = !(a.state[v] & (ST_DOWN | ST_SATED)) && a.seenpop[vi] < a.done_at[v] && !hub && e > b;
       if constexpr ((MODE & 3) == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
       if constexpr ((MODE & 3) == SCAN_PRE) {
         // sparse filtered rounds: every lane probes the in-list of its own
@@ -396,9 +415,17 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
     while (m) {
       const int k = __ffsll((long long)m) - 1;
       m &= m - 1;
-      const int64_t i = base + k;
-      const int v = uniform((int)(a.vbegin + i));
-      const int64_t vb = L.rp[k], ve = L.rp[k + 1];   // staged by the lane phase
+      int64_t i = base + k;
+      int v = uniform((int)(a.vbegin + i));
+      const int64_t vb = L.rp[k];   // staged by the lane phase
+      int64_t ve;
+      if constexpr (LIST) {
+        v = uniform(L.vid[k]);
+        i = v - a.vbegin;
+        ve = L.re[k];
+      } else {
+        ve = L.rp[k + 1];
+      }
       const uint32_t sv_slot = (uint32_t)__builtin_amdgcn_readlane((int)slot_of, k);
       u64x2 acc = {0, 0}, want = {0, 0};
       // early-exit rounds: the first pass's column ids are loaded beside the
@@ -472,9 +499,25 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
                                                   full);
     }
     alive_flush<W>(a, L.alive, lane);
-    commit_vertices(a, L, li, need, st);
+    commit_vertices(a, L, vi, need, st);
     if constexpr (ALIVE) {
-      if (sat && ((sat >> lane) & 1ull)) a.state[a.vbegin + li] |= ST_SATED;
+      if (sat && ((sat >> lane) & 1ull)) a.state[a.vbegin + vi] |= ST_SATED;
+    }
+    // the next round's list: receivers still neither done
+    // nor sated -- the set only shrinks (seenpop grows, done_at and the down /
+    // sated marks only move one way), so it holds every later receiver
+    if constexpr (EMIT) {
+      if (a.ulist_next) {
+        const bool surv = need && !((sat >> lane) & 1ull) &&
+                          a.seenpop[vi] < a.done_at[a.vbegin + vi];   // (commit_vertices' sum: this lane's own write)
+        const u64 sm = __ballot(surv);
+        if (sm) {
+          uint32_t p0 = 0;
+          if (lane == 0) p0 = (uint32_t)atomicAdd(a.stats + S_ULIST, (u64)__popcll(sm));
+          p0 = (uint32_t)__shfl((int)p0, 0);
+          if (surv) a.ulist_next[p0 + lane_rank(sm)] = (int32_t)vi;
+        }
+      }
     }
   }
   flush_stats<EWAVES>(st, a.partial);
@@ -1300,6 +1343,21 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
       } else {
         if (ee) hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED, true>), grid, dim3(EBLOCK), 0, c->stream, a);
         else hipLaunchKernelGGL((k_expand_flat<W, SCAN_FILTERED, false>), grid, dim3(EBLOCK), 0, c->stream, a);
+      }
+    }
+  } else if (W == 64 && a.ulist) {   // receiver-list round (launch_expand): waves for the listed vertices
+    if constexpr (W == 64) {
+      const dim3 lgrid(grid_for(a.ulist_n, per_block));
+      const bool unf = mode == SCAN_UNFILTERED;
+      if (a.alive && a.early_exit) {
+        if (unf) hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE | SCAN_LIST>), lgrid, dim3(EBLOCK), 0, c->stream, a);
+        else hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_ALIVE | SCAN_LIST>), lgrid, dim3(EBLOCK), 0, c->stream, a);
+      } else if (a.dprobe) {
+        if (unf) hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_DPROBE | SCAN_LIST>), lgrid, dim3(EBLOCK), 0, c->stream, a);
+        else hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_DPROBE | SCAN_LIST>), lgrid, dim3(EBLOCK), 0, c->stream, a);
+      } else {
+        if (unf) hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_LIST>), lgrid, dim3(EBLOCK), 0, c->stream, a);
+        else hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_LIST>), lgrid, dim3(EBLOCK), 0, c->stream, a);
       }
     }
   } else if (a.nloc > 0) {

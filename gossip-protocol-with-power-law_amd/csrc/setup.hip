@@ -209,6 +209,8 @@ static void free_state(Ctx* c) {
     dfree(&c->d_fpop[k]);
   }
   dfree(&c->d_sp); dfree(&c->d_ws);
+  dfree(&c->d_ulist[0]); dfree(&c->d_ulist[1]);
+  c->ulist_valid = false;
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_det_big); dfree(&c->d_det_pre); dfree(&c->d_det_live); dfree(&c->d_det_cur); dfree(&c->d_det_base);
@@ -522,6 +524,7 @@ void gp_destroy(gp_ctx* c) {
   free_rows(c);
   for (int k = 0; k < 2; ++k) { dfree(&c->d_frx[k]); dfree(&c->d_fpop[k]); }
   dfree(&c->d_sp); dfree(&c->d_ws);
+  dfree(&c->d_ulist[0]); dfree(&c->d_ulist[1]);
   dfree(&c->d_seenpop); dfree(&c->d_first); dfree(&c->d_digest);
   dfree(&c->d_state); dfree(&c->d_miss); dfree(&c->d_deg_live); dfree(&c->d_cand);
   dfree(&c->d_det_big); dfree(&c->d_det_pre); dfree(&c->d_det_live); dfree(&c->d_det_cur); dfree(&c->d_det_base);
@@ -822,6 +825,8 @@ int gp_reset(gp_ctx* c) {
   c->msg_forwards_valid = true;
   c->last_reports = 0;
   c->alias_active = c->alias_now = c->dprobe_now = false;
+  c->ulist_valid = c->ulist_emit_now = c->ulist_read_now = false;
+  c->ulist_valid = c->ulist_emit_now = c->ulist_read_now = false;
   shard_reset(c);
   GP_HIP(hipStreamSynchronize(s));
   return 0;

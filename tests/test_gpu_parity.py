@@ -1135,6 +1135,27 @@ def test_aliased_message_lists(pkg, oracle, mode):
     if mode == "adaptive":
         k = max(i for i, s in enumerate(st) if s["aliased"])
         assert any(s["mode"] == 1 for s in st[k + 1:]), "no push round after aliasing"
+    if mode == "pull":   # the last pulls take their receivers from the list the one before left
+        assert any(s["scan"] & 128 for s in st)
+    r["eng"].close()
+
+
+@pytest.mark.parametrize("push_ratio", [0.0, 10.0])
+@pytest.mark.parametrize("track_fwd", [0, 1])
+def test_receiver_lists_under_churn(pkg, oracle, push_ratio, track_fwd):
+    """Late W = 64 early-exit pulls under liveness: each
+    appends its receivers that are neither sated nor complete, and a pull
+    whose list is short launches waves for the listed vertices alone
+    (SCAN_LIST, scan bit 128) while k_mkbits counts every sender's sends.
+    Counters, first receipts, digests, coverage and the dead-node reports
+    equal the oracle's (Peer.py:298-313, Seed.py:387-391: crashes, 3-miss
+    detection and removal every round)."""
+    rp, col = oracle.chung_lu(150_000, 12, 2.4, 47)
+    g = pkg.CSR(150_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, 4096, seed=47)
+    r = _compare(pkg, oracle, g, origin, first=True, push_ratio=push_ratio, compact_rows=0, arc_mask_permille=0,
+                 track_fwd=track_fwd, churn=True, p_fail=0.01, churn_seed=9)
+    assert any(s["scan"] & 128 for s in r["stats"])
     r["eng"].close()
 
 
