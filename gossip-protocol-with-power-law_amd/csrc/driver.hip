@@ -597,7 +597,11 @@ static int launch_expand(Ctx* c) {
     c->arc_mask_now = c->prefilter_now = c->split_now = false;
     c->cml_read_now = c->cml_write_now = c->lines_now = c->lm_write_now = false;
   }
-  c->ulist_emit_now = list_ok && (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m && !c->arc_mask_now &&
+  // (only once the rounds thin out: last round's new bits under m/4 per
+  // vertex -- C4 round 4's survivors, 7.6 M, would make no list worth reading,
+  // and appending them cost the round 0.07 ms)
+  c->ulist_emit_now = list_ok && (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m &&
+                      (double)c->prev_new_bits * 4.0 < (double)c->n * (double)c->m && !c->arc_mask_now &&
                       !c->prefilter_now && !c->split_now && !c->cml_read_now && !c->cml_write_now && !c->lines_now;
   if (c->ulist_emit_now && !c->d_ulist[0]) {
     if (dalloc(&c->d_ulist[0], (size_t)c->n_alloc) != 0 || dalloc(&c->d_ulist[1], (size_t)c->n_alloc) != 0) {

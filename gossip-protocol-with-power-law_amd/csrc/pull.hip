@@ -201,6 +201,93 @@ __device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
   }
 }
 
+// The same four at a time, one per quarter-wave (W = 64, the done-probe
+// variants, i.e. the late rounds: C4 round 5's 7.5 M receivers are all done-
+// neighbour ones): a quarter-wave holds a whole row at 32 B per lane (words
+// 4ql .. 4ql + 3), so four receivers' seen and component rows are in flight
+// per round trip instead of two.  No liveness (no alive sets, no records).
+template <bool ALIAS, class LDS>
+__device__ __forceinline__ void dnb_quads(const ExpandArgs& a, LDS& L, u64 mq, int64_t base, uint32_t slot_of,
+                                          WaveStats& st) {
+  const int lane = threadIdx.x & 63, qd = lane >> 4, ql = lane & 15;
+  const bool alias = ALIAS && a.alias != 0;
+  while (mq) {
+    int kq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      kq[q] = -1;
+      if (mq) {
+        kq[q] = __ffsll((long long)mq) - 1;
+        mq &= mq - 1;
+      }
+    }
+    const int ks = qd == 0 ? kq[0] : qd == 1 ? kq[1] : qd == 2 ? kq[2] : kq[3];
+    const bool on = ks >= 0;
+    int64_t i = base + (on ? ks : 0);
+    int v = (int)(a.vbegin + i);
+    if constexpr (LDS::kList) {
+      v = on ? L.vid[ks] : 0;
+      i = v - a.vbegin;
+    }
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, on ? ks : 0);
+    u64x2 s0 = {0, 0}, s1 = {0, 0}, c0 = {0, 0}, c1 = {0, 0};
+    if (on) {
+      if (sv_slot != SLOT_NONE) {
+        const u64* r = a.slot[sv_slot] + (size_t)v * 64 + 4 * ql;
+        s0 = *reinterpret_cast<const u64x2*>(r);
+        s1 = *reinterpret_cast<const u64x2*>(r + 2);
+      }
+      const u64* cr = a.cmask + (size_t)L.mi[ks] * 64 + 4 * ql;
+      c0 = *reinterpret_cast<const u64x2*>(cr);
+      c1 = *reinterpret_cast<const u64x2*>(cr + 2);
+    }
+    const u64x2 n0 = c0 & ~s0, n1 = c1 & ~s1;
+    uint32_t tot = (uint32_t)(__popcll(n0.x) + __popcll(n0.y) + __popcll(n1.x) + __popcll(n1.y));
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
+    u64 t = 0;
+    if (on && tot) {
+      u64* out = a.slot[a.wslot] + (size_t)v * 64 + 4 * ql;
+      if (!alias) {
+        *reinterpret_cast<u64x2*>(out) = s0 | n0;
+        *reinterpret_cast<u64x2*>(out + 2) = s1 | n1;
+      }
+      if (a.frx_next) {
+        u64* f = a.frx_next + (size_t)v * 64 + 4 * ql;
+        *reinterpret_cast<u64x2*>(f) = n0;
+        *reinterpret_cast<u64x2*>(f + 2) = n1;
+      }
+      const u64 nw[4] = {n0.x, n0.y, n1.x, n1.y};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!nw[j]) continue;
+        if (a.first) set_first_bytes(a.first + (size_t)i * (64 * 64), 4 * ql + j, nw[j], (uint32_t)a.rr);
+        if (a.digest) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 4 * ql + j), nw[j]);
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) t ^= __shfl_xor(t, o);
+    if (ql == 0 && on && tot) {
+      L.tot[ks] = tot;
+      L.lmn[ks] = alias ? LMN_ALIAS : (uint8_t)0;   // (no line masks are written in early-exit rounds)
+      L.dig[ks] = t;
+    }
+    uint32_t nb = 0, nr = 0, nsr = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t tq = (uint32_t)__builtin_amdgcn_readlane((int)tot, 16 * q);
+      const uint32_t sq = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 16 * q);
+      nb += kq[q] >= 0 ? tq : 0u;
+      nr += (kq[q] >= 0 && tq) ? 1u : 0u;
+      nsr += (kq[q] >= 0 && sq != SLOT_NONE) ? 1u : 0u;
+    }
+    st.add(S_NEW_BITS, nb);
+    st.add(S_RECEIVERS, nr);
+    st.add(alias ? S_ALIASED : S_WRITTEN, nr);
+    st.add(S_SEEN_READ, nsr);
+  }
+}
+
 // main pull kernel: a wave owns 64 consecutive vertices.  The per-vertex
 // checks (sender accounting, down / done / hub / no in-arcs) run lane-parallel
 // with coalesced loads; the wave then scans, one receiver at a time, only the
@@ -405,7 +492,11 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
     if constexpr (W == 64) {
       if (mdn) {   // done in-neighbours: two receivers at a time, the rest below
         const u64 md = m & mdn;
-        dnb_pairs<W, ALIVE, ALIASABLE>(a, L, md, base, slot_of, st);
+#ifndef GP_DNB_QUADS
+#define GP_DNB_QUADS 1
+#endif
+        if constexpr (DPROBE && !ALIVE && GP_DNB_QUADS) dnb_quads<ALIASABLE>(a, L, md, base, slot_of, st);
+        else dnb_pairs<W, ALIVE, ALIASABLE>(a, L, md, base, slot_of, st);
         if constexpr (ALIVE) {   // they now hold every alive message of their component: sated too
           if (a.sate) sat |= md;
         }
