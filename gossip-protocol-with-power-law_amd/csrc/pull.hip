@@ -206,7 +206,7 @@ __device__ __forceinline__ void dnb_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
 // neighbour ones): a quarter-wave holds a whole row at 32 B per lane (words
 // 4ql .. 4ql + 3), so four receivers' seen and component rows are in flight
 // per round trip instead of two.  No liveness (no alive sets, no records).
-template <bool ALIAS, class LDS>
+template <bool ALIAS, bool ALIVE, class LDS>
 __device__ __forceinline__ void dnb_quads(const ExpandArgs& a, LDS& L, u64 mq, int64_t base, uint32_t slot_of,
                                           WaveStats& st) {
   const int lane = threadIdx.x & 63, qd = lane >> 4, ql = lane & 15;
@@ -240,6 +240,10 @@ __device__ __forceinline__ void dnb_quads(const ExpandArgs& a, LDS& L, u64 mq, i
       const u64* cr = a.cmask + (size_t)L.mi[ks] * 64 + 4 * ql;
       c0 = *reinterpret_cast<const u64x2*>(cr);
       c1 = *reinterpret_cast<const u64x2*>(cr + 2);
+      if (ALIVE && a.alive) {   // liveness: the sated neighbour's alive set
+        c0 &= *reinterpret_cast<const u64x2*>(a.alive + 4 * ql);
+        c1 &= *reinterpret_cast<const u64x2*>(a.alive + 4 * ql + 2);
+      }
     }
     const u64x2 n0 = c0 & ~s0, n1 = c1 & ~s1;
     uint32_t tot = (uint32_t)(__popcll(n0.x) + __popcll(n0.y) + __popcll(n1.x) + __popcll(n1.y));
@@ -261,6 +265,7 @@ __device__ __forceinline__ void dnb_quads(const ExpandArgs& a, LDS& L, u64 mq, i
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (!nw[j]) continue;
+        if (ALIVE && a.alive_next) atomicOr(&L.alive[4 * ql + j], nw[j]);   // (alive_add's words)
         if (a.first) set_first_bytes(a.first + (size_t)i * (64 * 64), 4 * ql + j, nw[j], (uint32_t)a.rr);
         if (a.digest) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 4 * ql + j), nw[j]);
       }
@@ -495,7 +500,9 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
 #ifndef GP_DNB_QUADS
 #define GP_DNB_QUADS 1
 #endif
-        if constexpr (DPROBE && !ALIVE && GP_DNB_QUADS) dnb_quads<ALIASABLE>(a, L, md, base, slot_of, st);
+        // (quads in the alive variants too: C5 round 5 11.95 -> 11.78 ms, but
+        // round 3, the same kernel, 73.8 -> 78.7 ms, profiles/r06_ab_quads_c5.txt)
+        if constexpr (DPROBE && !ALIVE && GP_DNB_QUADS) dnb_quads<ALIASABLE, false>(a, L, md, base, slot_of, st);
         else dnb_pairs<W, ALIVE, ALIASABLE>(a, L, md, base, slot_of, st);
         if constexpr (ALIVE) {   // they now hold every alive message of their component: sated too
           if (a.sate) sat |= md;
