@@ -94,8 +94,10 @@ __global__ __launch_bounds__(BLOCK) void k_mkbits(const uint32_t* __restrict__ f
     if (dbits) {
       bool d = false;
       if (v < n) {
-        if (sated) {
-          d = (sated[v] & (ST_SATED | ST_DOWN)) == ST_SATED;
+        if (sated) {   // (a complete up vertex holds every alive message too: pulls never mark it)
+          const uint8_t sv = sated[v];
+          const uint32_t t = done_at[v];
+          d = !(sv & ST_DOWN) && ((sv & ST_SATED) || (t != 0u && seenpop[v] == t));
         } else {
           const uint32_t t = done_at[v];
           d = t != 0u && seenpop[v] == t;

@@ -313,7 +313,10 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
   constexpr bool LIST = (MODE & SCAN_LIST) != 0;
   constexpr int SCAN = MODE & ~(SCAN_ALIVE | SCAN_DPROBE | SCAN_LIST);
   // the variants that can append this round's survivors to the next list
-  constexpr bool EMIT = W == 64 && (SCAN == SCAN_FILTERED || SCAN == SCAN_UNFILTERED);
+#ifndef GP_ULIST_EMIT
+#define GP_ULIST_EMIT 1
+#endif
+  constexpr bool EMIT = GP_ULIST_EMIT && W == 64 && (SCAN == SCAN_FILTERED || SCAN == SCAN_UNFILTERED);
   // the variants done-neighbour rounds without liveness launch: their complete
   // receivers may alias (a.alias) and their scans probe the done bitmap
   // (a.dprobe); the other variants compile neither
