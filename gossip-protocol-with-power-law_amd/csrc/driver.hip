@@ -520,7 +520,10 @@ static int launch_expand(Ctx* c) {
 #endif
   const bool list_ok = GP_ULIST && !c->mode_push && !c->local && c->nloc() == c->n_alloc && c->words == 64 &&
                        c->words > c->cfg.flat_max_words && c->cfg.compact_rows == 0 && c->early_exit_now;
-  c->ulist_read_now = list_ok && c->ulist_valid && c->ulist_n * 3 < c->n_alloc;
+#ifndef GP_ULIST_DIV
+#define GP_ULIST_DIV 3
+#endif
+  c->ulist_read_now = list_ok && c->ulist_valid && c->ulist_n * GP_ULIST_DIV < c->n_alloc;
   if (c->ulist_read_now)
     GP_HIP(hipMemsetAsync(c->d_fpop[c->cur ^ 1], 0, (size_t)c->nloc() * 4, c->stream));
   hipLaunchKernelGGL(k_mkbits, dim3(std::max(1, std::min(grid_for(c->n_alloc, BLOCK), c->cu_count * 8 * GS))),

@@ -396,7 +396,10 @@ enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PR
                                     a variant of its own: +4 VGPRs cost the unfiltered pull a wave */,
                 SCAN_LIST = 128 /* flag (k_expand, W >= 32, filtered / unfiltered): the waves take
                                    their receivers from a.ulist, the vertices that could still
-                                   receive (late rounds), not 64 consecutive ids */ };
+                                   receive (late rounds), not 64 consecutive ids */,
+                SCAN_QUADS = 256 /* flag (k_expand, W = 64): done-neighbour receivers four per wave
+                                    step (dnb_quads) without the done probe: the first aliasing
+                                    round */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads

@@ -311,7 +311,8 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
   constexpr bool ALIVE = (MODE & SCAN_ALIVE) != 0;
   constexpr bool DPROBE = (MODE & SCAN_DPROBE) != 0;
   constexpr bool LIST = (MODE & SCAN_LIST) != 0;
-  constexpr int SCAN = MODE & ~(SCAN_ALIVE | SCAN_DPROBE | SCAN_LIST);
+  constexpr bool QUADS = (MODE & SCAN_QUADS) != 0;
+  constexpr int SCAN = MODE & ~(SCAN_ALIVE | SCAN_DPROBE | SCAN_LIST | SCAN_QUADS);
   // the variants that can append this round's survivors to the next list
 #ifndef GP_ULIST_EMIT
 #define GP_ULIST_EMIT 1
@@ -505,7 +506,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
 #endif
         // (quads in the alive variants too: C5 round 5 11.95 -> 11.78 ms, but
         // round 3, the same kernel, 73.8 -> 78.7 ms, profiles/r06_ab_quads_c5.txt)
-        if constexpr (DPROBE && !ALIVE && GP_DNB_QUADS) dnb_quads<ALIASABLE, false>(a, L, md, base, slot_of, st);
+        if constexpr ((DPROBE || QUADS) && !ALIVE && GP_DNB_QUADS) dnb_quads<ALIASABLE, false>(a, L, md, base, slot_of, st);
         else dnb_pairs<W, ALIVE, ALIASABLE>(a, L, md, base, slot_of, st);
         if constexpr (ALIVE) {   // they now hold every alive message of their component: sated too
           if (a.sate) sat |= md;
@@ -1387,6 +1388,11 @@ __global__ __launch_bounds__(BLOCK) void k_park(const uint8_t* __restrict__ stat
   }
 }
 
+// the first aliasing round (alias without the done probe) runs the quads
+// variant of the unfiltered pull
+#ifndef GP_ALIAS_QUADS
+#define GP_ALIAS_QUADS 1
+#endif
 template <int W>
 static void launch_expand_w(Ctx* c, ExpandArgs a) {
   if (c->mode_push) {
@@ -1475,6 +1481,9 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
         else
           hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_DPROBE>), grid, dim3(EBLOCK), 0, c->stream, a);
       }
+    } else if (W == 64 && GP_ALIAS_QUADS && a.alias && mode == SCAN_UNFILTERED) {   // (the first aliasing round)
+      if constexpr (W == 64)
+        hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_QUADS>), grid, dim3(EBLOCK), 0, c->stream, a);
     } else if (mode == SCAN_UNFILTERED) {
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(EBLOCK), 0, c->stream, a);
     }
