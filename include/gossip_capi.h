@@ -93,7 +93,9 @@ typedef struct gp_round_stats {
                                split_deg pushed, receivers probe the gather-order
                                prefix of the others, §3.2); + 64: every scanned
                                arc probed the done bitmap (complete receivers
-                               alias their component row, `aliased`, §3.2)        */
+                               alias their component row, `aliased`, §3.2);
+                               + 128: the waves took their receivers from the
+                               list the previous round left (§3.5)                */
   double expand_ms;         /* device time of the expansion kernels (HIP events)     */
   double exchange_ms;       /* device time of the RCCL exchange (0 on 1 GPU)         */
   double round_ms;          /* device time of the whole round                        */
