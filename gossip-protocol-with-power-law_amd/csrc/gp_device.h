@@ -272,10 +272,10 @@ constexpr int PRE_MAX_DEG = 16;  // in-degree up to which the lane phase probes
 #define GP_WAVE_PRE_MAX 64
 #endif
 constexpr int WAVE_PRE_N = 4;   // (2 and 8 measured equal)
-template <bool PRE, bool CML, bool LIST = false>
+template <bool PRE, bool CML, bool LIST = false, bool PAIRS = false>
 struct WaveLdsT {
   static constexpr bool kPre = PRE, kCml = CML, kList = LIST;
-  u64 seen[64];         // early exit: the receiver's seen row (read once, reused by finish_row)
+  u64 seen[PAIRS ? 128 : 64];   // early exit: the receiver's seen row (read once, reused by finish_row; gather_pairs: two)
   int32_t idx[64];      // active neighbours of one pass
   uint32_t tot[64];     // k_expand: new bits of the wave's vertex k (committed after the loop)
   uint8_t lmn[64];      // k_expand: line mask of vertex k's new row (committed with tot)
@@ -293,7 +293,8 @@ struct WaveLdsT {
   int64_t re[LIST ? 64 : 1];      // SCAN_LIST: end of vertex k's in-list
 };
 using WaveLds = WaveLdsT<false, false>;
-#define LDS_OF(MODE) WaveLdsT<((MODE) & 3) == SCAN_PRE, ((MODE) & SCAN_CML) != 0, ((MODE) & SCAN_LIST) != 0>
+#define LDS_OF(MODE) \
+  WaveLdsT<((MODE) & 3) == SCAN_PRE, ((MODE) & SCAN_CML) != 0, ((MODE) & SCAN_LIST) != 0, ((MODE) & SCAN_QUADS) != 0>
 
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -398,8 +399,10 @@ enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PR
                                    their receivers from a.ulist, the vertices that could still
                                    receive (late rounds), not 64 consecutive ids */,
                 SCAN_QUADS = 256 /* flag (k_expand, W = 64): done-neighbour receivers four per wave
-                                    step (dnb_quads) without the done probe: the first aliasing
-                                    round */ };
+                                    step (dnb_quads) without the done probe, and (unfiltered, no
+                                    liveness) receivers of in-degree <= 32 two per step
+                                    (gather_pairs): the first aliasing round, near-done pulls,
+                                    alive pulls from the half-held round */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads

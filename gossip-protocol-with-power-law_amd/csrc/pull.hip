@@ -78,7 +78,10 @@ __device__ __forceinline__ void pair_finish(const ExpandArgs& a, LDS& L, int h, 
   const uint32_t tB = kB >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)tot, 32) : 0u;
   st.add(S_NEW_BITS, (u64)tA + (u64)tB);
   st.add(S_RECEIVERS, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
-  st.add(alias ? S_ALIASED : S_WRITTEN, (u64)((tA ? 1 : 0) + (tB ? 1 : 0)));
+  // (alias is per half: gather_pairs' receivers complete or not each on its own)
+  const bool aA = __builtin_amdgcn_readlane((int)alias, 0) != 0, aB = __builtin_amdgcn_readlane((int)alias, 32) != 0;
+  st.add(S_ALIASED, (u64)((tA && aA ? 1 : 0) + (tB && aB ? 1 : 0)));
+  st.add(S_WRITTEN, (u64)((tA && !aA ? 1 : 0) + (tB && !aB ? 1 : 0)));
 }
 
 // the seen row of a pair's receivers, loaded after a gather without early
@@ -293,6 +296,105 @@ __device__ __forceinline__ void dnb_quads(const ExpandArgs& a, LDS& L, u64 mq, i
   }
 }
 
+// Receivers of in-degree <= 32 two at a time, one per half-wave (W = 64, the
+// unfiltered SCAN_QUADS variants: near-done pulls, C4 round 4 / C5 rounds
+// 4-5, where a receiver lacks a few words and gathers ~8 rows).  A half loads
+// its receiver's column ids (one per lane), seen row and component row in one
+// round trip, then gathers GP_GPAIR_RIF rows at a time (a whole 512-B row per
+// half-wave instruction) until they cover its target (per-lane word skip as in
+// gather_rows_n).  The serial loop walks target -> rows -> rows one receiver
+// after the other; here two receivers' chains share each round trip.  Same
+// rows, commits and sated marks as the serial loop (returned: the sated
+// receivers, alive rounds).
+#ifndef GP_GPAIR_RIF
+#define GP_GPAIR_RIF 3
+#endif
+template <bool ALIVE, bool ALIAS, class LDS>
+__device__ __forceinline__ u64 gather_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
+                                            WaveStats& st) {
+  constexpr int W = 64;
+  const int lane = threadIdx.x & 63, h = lane >> 5, lw = lane & 31;
+  const bool ee = a.early_exit != 0;
+  u64 sat = 0;
+  while (mp) {
+    const int kA = __ffsll((long long)mp) - 1;
+    mp &= mp - 1;
+    int kB = -1;
+    if (mp) {
+      kB = __ffsll((long long)mp) - 1;
+      mp &= mp - 1;
+    }
+    const bool on = h == 0 || kB >= 0;
+    const int ks = (h && kB >= 0) ? kB : kA;
+    const int v = (int)(a.vbegin + base + ks);
+    const int64_t vb = L.rp[ks];
+    const int deg = on ? (int)(L.rp[ks + 1] - vb) : 0;   // <= 32 (the caller's mask)
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
+    u64x2 want = {0, 0};
+    if (lw < deg) L.idx[32 * h + lw] = a.gcol[vb + lw];   // (this pair's column ids: half h at 32h)
+    {
+      u64x2 sv = {0, 0};
+      if (on) {
+        if (sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
+        if (ee) {
+          u64x2 cm = load_piece<W>(a.cmask, L.mi[ks], lw);
+          if (ALIVE && a.alive) cm &= load_piece<W>(a.alive, 0, lw);
+          want = cm & ~sv;
+        }
+      }
+      L.seen[64 * h + 2 * lw] = sv.x;   // (parked for the commit: registers for the rows in flight)
+      L.seen[64 * h + 2 * lw + 1] = sv.y;
+    }
+    const int dA = __builtin_amdgcn_readlane(deg, 0), dB = __builtin_amdgcn_readlane(deg, 32);
+    const uint32_t sA = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 0);
+    const uint32_t sB = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 32);
+    st.add(S_ARCS, (u64)(dA + dB));
+    st.add(S_SEEN_READ, (u64)((sA != SLOT_NONE ? 1 : 0) + (kB >= 0 && sB != SLOT_NONE ? 1 : 0)));
+    bool live = on && (!ee || (want.x | want.y) != 0ull);   // this lane's words still miss messages
+    u64x2 acc = {0, 0};
+    u64 rows = 0, pieces = 0;
+    for (int k0 = 0; k0 < max(dA, dB); k0 += GP_GPAIR_RIF) {
+      const u64 lb = __ballot(live);
+      if (lb == 0ull) break;
+      // one branch for the batch: a lane past its receiver's last arc loads
+      // that last row again (same line, already requested: no HBM bytes),
+      // which keeps the RIF loads unconditional inside it
+      if (live && k0 < deg) {
+        u64x2 r[GP_GPAIR_RIF];
+#pragma unroll
+        for (int q = 0; q < GP_GPAIR_RIF; ++q) r[q] = load_piece<W>(a.rows, L.idx[32 * h + min(k0 + q, deg - 1)], lw);
+#pragma unroll
+        for (int q = 0; q < GP_GPAIR_RIF; ++q) acc |= r[q];
+      }
+#pragma unroll
+      for (int q = 0; q < GP_GPAIR_RIF; ++q) pieces += line_pieces<W>(__ballot(live && k0 + q < deg));
+      if (lb & 0xFFFFFFFFull) rows += (u64)min(GP_GPAIR_RIF, max(dA - k0, 0));
+      if (lb >> 32) rows += (u64)min(GP_GPAIR_RIF, max(dB - k0, 0));
+      if (ee) {
+        const u64x2 miss = want & ~acc;
+        live = live && (miss.x | miss.y) != 0ull;
+      }
+    }
+    st.add(S_GATHERED, rows);
+    st.add(S_ROW_BYTES, pieces * 16ull);
+    // a half whose rows covered its whole target: the receiver completes its
+    // component (alias rounds: it commits SLOT_CMASK) or, under liveness,
+    // holds every alive message it lacked (sated)
+    const u64x2 rem = want & ~acc;
+    const u64 rb = __ballot(on && (rem.x | rem.y) != 0ull);
+    const bool full = ((rb >> (32 * h)) & 0xFFFFFFFFull) == 0ull;
+    if constexpr (ALIVE) {
+      if (a.sate && ee && a.alive) {
+        if (!(rb & 0xFFFFFFFFull)) sat |= 1ull << kA;
+        if (kB >= 0 && !(rb >> 32)) sat |= 1ull << kB;
+      }
+    }
+    const u64x2 sv = {L.seen[64 * h + 2 * lw], L.seen[64 * h + 2 * lw + 1]};
+    pair_finish<W>(a, L, h, lw, on, ks, kB, base + ks, v, acc, sv, st, ALIAS && a.alias != 0 && ee && full);
+  }
+  return sat;
+}
+
 // main pull kernel: a wave owns 64 consecutive vertices.  The per-vertex
 // checks (sender accounting, down / done / hub / no in-arcs) run lane-parallel
 // with coalesced loads; the wave then scans, one receiver at a time, only the
@@ -322,6 +424,15 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
   // receivers may alias (a.alias) and their scans probe the done bitmap
   // (a.dprobe); the other variants compile neither
   constexpr bool ALIASABLE = W == 64 && !ALIVE && (SCAN == SCAN_FILTERED || SCAN == SCAN_UNFILTERED);
+  // the variants whose receivers of in-degree <= 32 go two at a time
+  // (gather_pairs): the unfiltered near-done pulls without liveness
+  // (SCAN_QUADS; C4 round 4 6.93-7.02 -> 6.61-6.65 ms, 80 VGPRs; in the alive
+  // one C5 rounds 4-5 gained nothing: their receivers scan to the end,
+  // profiles/r06_ab_gather_pairs.txt)
+#ifndef GP_GATHER_PAIRS
+#define GP_GATHER_PAIRS 1
+#endif
+  constexpr bool GPAIRS = GP_GATHER_PAIRS && W == 64 && QUADS && !ALIVE && SCAN == SCAN_UNFILTERED && !LIST;
   WaveStats st;
   ws_zero<EWAVES>(st);
   const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * 64;
@@ -347,6 +458,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
     u64 sends = 0;
     uint32_t slot_of = SLOT_NONE;
     uint32_t pre_arcs = 0;   // SCAN_PRE: arcs the lane phase scanned
+    bool small = false;      // GPAIRS: in-degree <= 32
     if (valid) {
       const int v = (int)(a.vbegin + vi);
       if constexpr (!LIST) {
@@ -364,6 +476,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
       }
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
       need = !(a.state[v] & (ST_DOWN | ST_SATED)) && a.seenpop[vi] < a.done_at[v] && !hub && e > b;
+      if constexpr (GPAIRS) small = e - b <= 32;
       if constexpr ((MODE & 3) == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
       if constexpr ((MODE & 3) == SCAN_PRE) {
         // sparse filtered rounds: every lane probes the in-list of its own
@@ -506,12 +619,21 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
 #endif
         // (quads in the alive variants too: C5 round 5 11.95 -> 11.78 ms, but
         // round 3, the same kernel, 73.8 -> 78.7 ms, profiles/r06_ab_quads_c5.txt)
-        if constexpr ((DPROBE || QUADS) && !ALIVE && GP_DNB_QUADS) dnb_quads<ALIASABLE, false>(a, L, md, base, slot_of, st);
+        // (in the alive SCAN_QUADS variant, which only the half-held rounds
+        // launch, they pay: C5 round 5 12.2 -> 11.8 ms, r06_ab_gather_pairs.txt)
+        if constexpr ((DPROBE || QUADS) && GP_DNB_QUADS) dnb_quads<ALIASABLE, ALIVE>(a, L, md, base, slot_of, st);
         else dnb_pairs<W, ALIVE, ALIASABLE>(a, L, md, base, slot_of, st);
         if constexpr (ALIVE) {   // they now hold every alive message of their component: sated too
           if (a.sate) sat |= md;
         }
         m &= ~md;
+      }
+    }
+    if constexpr (GPAIRS) {   // low in-degree receivers two at a time, the rest below
+      const u64 mg = m & __ballot(small);
+      if (mg) {
+        sat |= gather_pairs<ALIVE, ALIASABLE>(a, L, mg, base, slot_of, st);
+        m &= ~mg;
       }
     }
     while (m) {
@@ -1389,9 +1511,20 @@ __global__ __launch_bounds__(BLOCK) void k_park(const uint8_t* __restrict__ stat
 }
 
 // the first aliasing round (alias without the done probe) runs the quads
-// variant of the unfiltered pull
+// variant of the unfiltered pull (done-neighbour receivers four at a time,
+// low in-degree ones two at a time), and so do the other unfiltered pulls
+// once most messages are held: near-done rounds without liveness
+// (GP_NEAR_QUADS) and, under liveness, the alive early-exit pulls from the
+// round that starts with half the messages held (GP_ALIVE_QUADS: C5 rounds
+// 4-5; round 3, the dense one, keeps the plain alive variant)
 #ifndef GP_ALIAS_QUADS
 #define GP_ALIAS_QUADS 1
+#endif
+#ifndef GP_NEAR_QUADS
+#define GP_NEAR_QUADS 1
+#endif
+#ifndef GP_ALIVE_QUADS
+#define GP_ALIVE_QUADS 1
 #endif
 template <int W>
 static void launch_expand_w(Ctx* c, ExpandArgs a) {
@@ -1471,9 +1604,16 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     const dim3 grid(grid_for(a.nloc, per_block));
     bool alive_ee = false;   // unfiltered under liveness (parked rows) with early exit
     if constexpr (W >= 32) alive_ee = mode == SCAN_UNFILTERED && a.alive && a.early_exit;
+    const bool half_held = (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m;
     if (alive_ee) {
-      if constexpr (W >= 32)
+      if constexpr (W == 64) {
+        if (GP_ALIVE_QUADS && half_held)
+          hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE | SCAN_QUADS>), grid, dim3(EBLOCK), 0, c->stream, a);
+        else
+          hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE>), grid, dim3(EBLOCK), 0, c->stream, a);
+      } else if constexpr (W >= 32) {
         hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_ALIVE>), grid, dim3(EBLOCK), 0, c->stream, a);
+      }
     } else if (W == 64 && a.dprobe) {   // (done-probe rounds: filtered or unfiltered, launch_expand)
       if constexpr (W == 64) {
         if (mode == SCAN_UNFILTERED)
@@ -1481,7 +1621,8 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
         else
           hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_DPROBE>), grid, dim3(EBLOCK), 0, c->stream, a);
       }
-    } else if (W == 64 && GP_ALIAS_QUADS && a.alias && mode == SCAN_UNFILTERED) {   // (the first aliasing round)
+    } else if (W == 64 && mode == SCAN_UNFILTERED &&
+               ((GP_ALIAS_QUADS && a.alias) || (GP_NEAR_QUADS && a.near_done))) {   // (the first aliasing round)
       if constexpr (W == 64)
         hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_QUADS>), grid, dim3(EBLOCK), 0, c->stream, a);
     } else if (mode == SCAN_UNFILTERED) {
