@@ -480,8 +480,23 @@ static int launch_expand(Ctx* c) {
   // once most messages are held (before that hardly any vertex is done, and
   // the probes only cost); the done bitmap comes with the activity bitmap (one
   // context: seenpop and done_at share the vertex index)
+  // Narrow rows (W = 8 / 16: the message shards of 4- and 8-GPU jobs) take the
+  // per-receiver kernel instead of the flat one in the thin late rounds (under
+  // 1/GP_NARROW_ND_DIV of the n x m bits still missing): its receivers go
+  // eight / sixteen per wave step (dnb_groups, gather_groups), while the flat
+  // kernel keeps the dense rounds, the last of which leaves a shard ~1 % short
+#ifndef GP_NARROW_ND
+#define GP_NARROW_ND 1
+#endif
+#ifndef GP_NARROW_ND_DIV
+#define GP_NARROW_ND_DIV 16
+#endif
+  const double nm = (double)c->n * (double)c->m;
+  c->narrow_pr_now = GP_NARROW_ND && (c->words == 8 || c->words == 16) && c->words <= c->cfg.flat_max_words &&
+                     c->early_exit_now && !c->mode_push && !c->liveness_active && !c->local &&
+                     c->nloc() == c->n_alloc && (nm - (double)c->held_bits) * GP_NARROW_ND_DIV < nm;
   c->dnb_now = c->early_exit_now && !c->mode_push && !c->liveness_active && !c->local &&
-               c->nloc() == c->n_alloc && c->words > c->cfg.flat_max_words &&
+               c->nloc() == c->n_alloc && (c->words > c->cfg.flat_max_words || c->narrow_pr_now) &&
                (double)c->held_bits * 2.0 >= (double)c->n * (double)c->m;
   // With liveness the done bitmap is the sated marks (up and sated: holds every
   // alive message of its component; k_mkbits): a receiver with such an

@@ -156,6 +156,7 @@ struct Ctx {
   // last round (done in-neighbours)
   u64* d_dbits = nullptr;
   bool dnb_now = false;             // this round's pull reads d_dbits
+  bool narrow_pr_now = false;       // W = 8 / 16 near-done pull on the per-receiver kernel (launch_expand)
   int32_t sate_since = -1;          // first round that marked sated vertices (-1: none yet this run)
   // [n_alloc] line masks (W = 64): bit l = 128-B line l of v's
   // row in this round's slot holds a nonzero word; 0 = not a sender.  Built by

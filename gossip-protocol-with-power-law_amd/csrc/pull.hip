@@ -296,6 +296,243 @@ __device__ __forceinline__ void dnb_quads(const ExpandArgs& a, LDS& L, u64 mq, i
   }
 }
 
+// W = 32 rows (two-rank message shards): receivers four per wave step, one
+// per 16-lane group (a 256-B row at 16 B per lane, the load_piece layout of
+// group g = lane / 16), where the serial loop took them one at a time -- the
+// done-neighbour receivers (dnb_groups: the N = 2 job's slow rank ran 7.5 M
+// of them in round 5 at 3.1 ms) and the prefiltered ones of sparse rounds
+// (pre_groups).  group_finish commits like finish_row (deferred per-vertex
+// words, L.tot / L.dig).
+#ifndef GP_DNB_GROUPS
+#define GP_DNB_GROUPS 1
+#endif
+#ifndef GP_PRE_GROUPS
+#define GP_PRE_GROUPS 1
+#endif
+template <int W>
+struct Groups {
+  static constexpr int LG = Geo<W>::LPR;   // lanes per row
+  static constexpr int NG = 64 / LG;       // receivers per step
+  static_assert(Geo<W>::WPL == 2 && NG >= 2 && NG <= 16, "16-B pieces, two to sixteen rows per wave");
+};
+
+// the next NG receivers of mq (kq[q] = -1: none); returns group gq's
+template <int NG>
+__device__ __forceinline__ int take_group(u64& mq, int (&kq)[NG], int gq) {
+  int ks = -1;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    kq[q] = -1;
+    if (mq) {
+      kq[q] = __ffsll((long long)mq) - 1;
+      mq &= mq - 1;
+    }
+    if (q == gq) ks = kq[q];
+  }
+  return ks;
+}
+
+template <int W, class LDS>
+__device__ __forceinline__ void group_finish(const ExpandArgs& a, LDS& L, int lw, bool on, int ks,
+                                             const int (&kq)[Groups<W>::NG], int64_t i, int v, u64x2 acc,
+                                             u64x2 sv, WaveStats& st) {
+  constexpr int LG = Groups<W>::LG, NG = Groups<W>::NG;
+  const u64x2 nw = acc & ~sv;
+  uint32_t tot = (uint32_t)(__popcll(nw.x) + __popcll(nw.y));
+#pragma unroll
+  for (int o = LG / 2; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
+  u64 t = 0;
+  if (on && tot) {
+    alive_add<W>(a, L, lw, nw);
+    store_piece<W>(a.slot[a.wslot], v, lw, sv | nw);
+    if (a.frx_next) store_piece<W>(a.frx_next, v, lw, nw);
+    if (a.first) {
+      uint8_t* row = a.first + (size_t)i * (W * 64);
+      if (nw.x) set_first_bytes(row, 2 * lw, nw.x, (uint32_t)a.rr);
+      if (nw.y) set_first_bytes(row, 2 * lw + 1, nw.y, (uint32_t)a.rr);
+    }
+    if (a.digest) {
+      if (nw.x) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 2 * lw), nw.x);
+      if (nw.y) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 2 * lw + 1), nw.y);
+    }
+  }
+#pragma unroll
+  for (int o = LG / 2; o > 0; o >>= 1) t ^= __shfl_xor(t, o);
+  if (lw == 0 && on && tot) {
+    L.tot[ks] = tot;
+    L.lmn[ks] = 0;   // (line masks: W = 64 only)
+    L.dig[ks] = t;
+  }
+  uint32_t nb = 0, nr = 0;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const uint32_t tq = (uint32_t)__builtin_amdgcn_readlane((int)tot, LG * q);
+    nb += kq[q] >= 0 ? tq : 0u;
+    nr += (kq[q] >= 0 && tq) ? 1u : 0u;
+  }
+  st.add(S_NEW_BITS, nb);
+  st.add(S_RECEIVERS, nr);
+  st.add(S_WRITTEN, nr);
+}
+
+// groups whose receiver's seen row was read (S_SEEN_READ): on[q] && slot[q] != SLOT_NONE
+template <int W>
+__device__ __forceinline__ uint32_t group_seen_reads(const int (&kq)[Groups<W>::NG], uint32_t sv_slot, u64 read) {
+  constexpr int LG = Groups<W>::LG, NG = Groups<W>::NG;
+  uint32_t n = 0;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const uint32_t sq = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, LG * q);
+    n += (kq[q] >= 0 && sq != SLOT_NONE && ((read >> (LG * q)) & 1ull)) ? 1u : 0u;
+  }
+  return n;
+}
+
+template <int W, bool ALIVE, class LDS>
+__device__ __forceinline__ void dnb_groups(const ExpandArgs& a, LDS& L, u64 mq, int64_t base, uint32_t slot_of,
+                                           WaveStats& st) {
+  constexpr int LG = Groups<W>::LG, NG = Groups<W>::NG;
+  const int lane = threadIdx.x & 63, gq = lane / LG, lw = lane % LG;
+  while (mq) {
+    int kq[NG];
+    const int ks = take_group<NG>(mq, kq, gq);
+    const bool on = ks >= 0;
+    int64_t i = base + (on ? ks : 0);
+    int v = (int)(a.vbegin + i);
+    if constexpr (LDS::kList) {
+      v = on ? L.vid[ks] : 0;
+      i = v - a.vbegin;
+    }
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, on ? ks : 0);
+    u64x2 sv = {0, 0}, cm = {0, 0};
+    if (on) {
+      if (sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
+      cm = load_piece<W>(a.cmask, L.mi[ks], lw);
+      if (ALIVE && a.alive) cm &= load_piece<W>(a.alive, 0, lw);   // liveness: the sated neighbour's alive set
+    }
+    st.add(S_SEEN_READ, group_seen_reads<W>(kq, sv_slot, ~0ull));
+    group_finish<W>(a, L, lw, on, ks, kq, i, v, cm & ~sv, sv, st);
+  }
+}
+
+// SCAN_PRE rounds without early exit: the receivers whose active
+// in-neighbours the lane phase staged (L.pre, at most PRE_IDS), four at a time
+template <int W, class LDS>
+__device__ __forceinline__ void pre_groups(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
+                                           WaveStats& st) {
+  constexpr int LG = Groups<W>::LG, NG = Groups<W>::NG;
+  const int lane = threadIdx.x & 63, gq = lane / LG, lw = lane % LG;
+  while (mp) {
+    int kq[NG];
+    const int ks = take_group<NG>(mp, kq, gq);
+    const bool on = ks >= 0;
+    const int64_t i = base + (on ? ks : 0);
+    const int v = (int)(a.vbegin + i);
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, on ? ks : 0);
+    const int np = on ? (int)L.np[ks] : 0;
+    int nmax = 0;
+    uint32_t rows = 0;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const int nq = __builtin_amdgcn_readlane(np, LG * q);
+      nmax = max(nmax, nq);
+      rows += (uint32_t)nq;
+    }
+    u64x2 acc = {0, 0};
+    for (int q0 = 0; q0 < nmax; q0 += GP_PAIR_RIF) {
+      if (q0 < np) {   // (one branch per batch; past the last row a lane reloads it: same line, in flight)
+        u64x2 r[GP_PAIR_RIF];
+#pragma unroll
+        for (int q = 0; q < GP_PAIR_RIF; ++q) r[q] = load_piece<W>(a.rows, L.pre[ks][min(q0 + q, np - 1)], lw);
+#pragma unroll
+        for (int q = 0; q < GP_PAIR_RIF; ++q) acc |= r[q];
+      }
+    }
+    st.add(S_GATHERED, (u64)rows);
+    st.add(S_ROW_BYTES, (u64)rows * (u64)(8 * W));
+    // the seen row only where the gather found something (pair_seen)
+    const u64 bz = __ballot(on && (acc.x | acc.y) != 0ull);
+    u64 gz = 0;   // bit LG * q: group q gathered a nonzero word
+#pragma unroll
+    for (int q = 0; q < NG; ++q)
+      if ((bz >> (LG * q)) & ((1ull << LG) - 1ull)) gz |= 1ull << (LG * q);
+    u64x2 sv = {0, 0};
+    if (((gz >> (LG * gq)) & 1ull) && sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
+    st.add(S_SEEN_READ, group_seen_reads<W>(kq, sv_slot, gz));
+    group_finish<W>(a, L, lw, on, ks, kq, i, v, acc, sv, st);
+  }
+}
+
+// rows in flight per receiver of gather_groups / gather_pairs
+#ifndef GP_GPAIR_RIF
+#define GP_GPAIR_RIF 3
+#endif
+
+// W = 32 near-done unfiltered pulls: receivers of in-degree <= 16 four per
+// wave step, one per 16-lane group (gather_pairs' scheme at a 256-B row per
+// group-instruction): column ids, seen and component rows in one round trip,
+// then GP_GPAIR_RIF rows per group in flight until the target is covered.
+template <int W, class LDS>
+__device__ __forceinline__ void gather_groups(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
+                                              WaveStats& st) {
+  constexpr int LG = Groups<W>::LG, NG = Groups<W>::NG;
+  const int lane = threadIdx.x & 63, gq = lane / LG, lw = lane % LG;
+  const bool ee = a.early_exit != 0;
+  while (mp) {
+    int kq[NG];
+    const int ks = take_group<NG>(mp, kq, gq);
+    const bool on = ks >= 0;
+    const int64_t i = base + (on ? ks : 0);
+    const int v = (int)(a.vbegin + i);
+    const int64_t vb = L.rp[on ? ks : 0];
+    const int deg = on ? (int)(L.rp[ks + 1] - vb) : 0;   // <= LG (the caller's mask)
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, on ? ks : 0);
+    if (lw < deg) L.idx[LG * gq + lw] = a.gcol[vb + lw];
+    u64x2 sv = {0, 0}, want = {0, 0};
+    if (on) {
+      if (sv_slot != SLOT_NONE) sv = load_piece<W>(a.slot[sv_slot], v, lw);
+      if (ee) want = load_piece<W>(a.cmask, L.mi[ks], lw) & ~sv;
+    }
+    wave_sync_lds();
+    int dq[NG], dmax = 0, arcs = 0;
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      dq[q] = __builtin_amdgcn_readlane(deg, LG * q);
+      dmax = max(dmax, dq[q]);
+      arcs += dq[q];
+    }
+    st.add(S_ARCS, (u64)arcs);
+    st.add(S_SEEN_READ, group_seen_reads<W>(kq, sv_slot, ~0ull));
+    bool live = on && (!ee || (want.x | want.y) != 0ull);
+    u64x2 acc = {0, 0};
+    u64 rows = 0, pieces = 0;
+    for (int k0 = 0; k0 < dmax; k0 += GP_GPAIR_RIF) {
+      const u64 lb = __ballot(live);
+      if (lb == 0ull) break;
+      if (live && k0 < deg) {   // (one branch per batch, gather_pairs)
+        u64x2 r[GP_GPAIR_RIF];
+#pragma unroll
+        for (int q = 0; q < GP_GPAIR_RIF; ++q) r[q] = load_piece<W>(a.rows, L.idx[LG * gq + min(k0 + q, deg - 1)], lw);
+#pragma unroll
+        for (int q = 0; q < GP_GPAIR_RIF; ++q) acc |= r[q];
+      }
+#pragma unroll
+      for (int q = 0; q < GP_GPAIR_RIF; ++q) pieces += line_pieces<W>(__ballot(live && k0 + q < deg));
+#pragma unroll
+      for (int q = 0; q < NG; ++q)
+        if ((lb >> (LG * q)) & ((1ull << LG) - 1ull)) rows += (u64)min(GP_GPAIR_RIF, max(dq[q] - k0, 0));
+      if (ee) {
+        const u64x2 miss = want & ~acc;
+        live = live && (miss.x | miss.y) != 0ull;
+      }
+    }
+    st.add(S_GATHERED, rows);
+    st.add(S_ROW_BYTES, pieces * 16ull);
+    wave_sync_lds();   // (the next step's column ids overwrite L.idx)
+    group_finish<W>(a, L, lw, on, ks, kq, i, v, acc, sv, st);
+  }
+}
+
 // Receivers of in-degree <= 32 two at a time, one per half-wave (W = 64, the
 // unfiltered SCAN_QUADS variants: near-done pulls, C4 round 4 / C5 rounds
 // 4-5, where a receiver lacks a few words and gathers ~8 rows).  A half loads
@@ -306,9 +543,6 @@ __device__ __forceinline__ void dnb_quads(const ExpandArgs& a, LDS& L, u64 mq, i
 // after the other; here two receivers' chains share each round trip.  Same
 // rows, commits and sated marks as the serial loop (returned: the sated
 // receivers, alive rounds).
-#ifndef GP_GPAIR_RIF
-#define GP_GPAIR_RIF 3
-#endif
 template <bool ALIVE, bool ALIAS, class LDS>
 __device__ __forceinline__ u64 gather_pairs(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
                                             WaveStats& st) {
@@ -332,6 +566,7 @@ __device__ __forceinline__ u64 gather_pairs(const ExpandArgs& a, LDS& L, u64 mp,
     const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, ks);
     u64x2 want = {0, 0};
     if (lw < deg) L.idx[32 * h + lw] = a.gcol[vb + lw];   // (this pair's column ids: half h at 32h)
+    wave_sync_lds();
     {
       u64x2 sv = {0, 0};
       if (on) {
@@ -389,6 +624,7 @@ __device__ __forceinline__ u64 gather_pairs(const ExpandArgs& a, LDS& L, u64 mp,
         if (kB >= 0 && !(rb >> 32)) sat |= 1ull << kB;
       }
     }
+    wave_sync_lds();   // (the next pair's column ids overwrite L.idx)
     const u64x2 sv = {L.seen[64 * h + 2 * lw], L.seen[64 * h + 2 * lw + 1]};
     pair_finish<W>(a, L, h, lw, on, ks, kB, base + ks, v, acc, sv, st, ALIAS && a.alias != 0 && ee && full);
   }
@@ -433,6 +669,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
 #define GP_GATHER_PAIRS 1
 #endif
   constexpr bool GPAIRS = GP_GATHER_PAIRS && W == 64 && QUADS && !ALIVE && SCAN == SCAN_UNFILTERED && !LIST;
+  constexpr bool GGROUPS = GP_GATHER_PAIRS && (W == 32 || W == 16 || W == 8) && QUADS && !ALIVE && SCAN == SCAN_UNFILTERED && !LIST;
   WaveStats st;
   ws_zero<EWAVES>(st);
   const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * 64;
@@ -477,6 +714,7 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
       const bool hub = e - b > a.hub_thr;   // split over waves by the hub kernels
       need = !(a.state[v] & (ST_DOWN | ST_SATED)) && a.seenpop[vi] < a.done_at[v] && !hub && e > b;
       if constexpr (GPAIRS) small = e - b <= 32;
+      if constexpr (GGROUPS) small = e - b <= Geo<W>::LPR;
       if constexpr ((MODE & 3) == SCAN_MASKED) need = need && mask_any(a.amask, b, e);
       if constexpr ((MODE & 3) == SCAN_PRE) {
         // sparse filtered rounds: every lane probes the in-list of its own
@@ -609,6 +847,12 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
         pre_pairs<W>(a, L, mp, base, slot_of, st);
         m &= ~mp;
       }
+    } else if constexpr ((W == 32 || W == 16 || W == 8) && GP_PRE_GROUPS && (MODE & 3) == SCAN_PRE) {
+      if (!ee) {   // four (eight) at a time (pre_groups)
+        const u64 mp = m & __ballot(need && L.np[lane] != 0xFFu);
+        pre_groups<W>(a, L, mp, base, slot_of, st);
+        m &= ~mp;
+      }
     }
     u64 sat = 0;   // receivers of this wave found sated (alive rounds)
     if constexpr (W == 64) {
@@ -628,11 +872,27 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
         }
         m &= ~md;
       }
+    } else if constexpr ((W == 32 || W == 16 || W == 8) && GP_DNB_GROUPS) {
+      if (mdn) {   // done in-neighbours, four (eight) at a time (dnb_groups)
+        const u64 md = m & mdn;
+        dnb_groups<W, ALIVE>(a, L, md, base, slot_of, st);
+        if constexpr (ALIVE) {
+          if (a.sate) sat |= md;
+        }
+        m &= ~md;
+      }
     }
     if constexpr (GPAIRS) {   // low in-degree receivers two at a time, the rest below
       const u64 mg = m & __ballot(small);
       if (mg) {
         sat |= gather_pairs<ALIVE, ALIASABLE>(a, L, mg, base, slot_of, st);
+        m &= ~mg;
+      }
+    }
+    if constexpr (GGROUPS) {   // W = 32: low in-degree receivers four at a time
+      const u64 mg = m & __ballot(small);
+      if (mg) {
+        gather_groups<W>(a, L, mg, base, slot_of, st);
         m &= ~mg;
       }
     }
@@ -1541,14 +1801,20 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
     hipLaunchKernelGGL(k_fixup_rows<W>, dim3(std::min(grid_for((c->n_alloc + 63) / 64, WAVES), c->cu_count * 8 * GS)),
                        dim3(BLOCK), 0, c->stream,
                        c->d_abits, c->d_ws, c->d_slot[c->cur], c->cur, c->n_alloc);
-  // W = 32 rows take the per-receiver kernel, except in dense near-done rounds
-  // (most messages held, last round's new bits >= m/4 per vertex): there the
-  // flat kernel's 2-arc prefix pass completes most receivers from their hub
-  // rows (2048-message shard round 4: 10.2 -> 6.6 ms; round 5, with m/16,
-  // went 3.2 -> 4.2 ms, hence m/4)
-  const bool flat_nd = W == 32 && c->cfg.flat_max_words > 0 && a.near_done &&
+  // W = 32 rows take the per-receiver kernel.  GP_FLAT_ND = 1 sends dense
+  // near-done rounds (most messages held, last round's new bits >= m/4 per
+  // vertex) to the flat kernel, whose 2-arc prefix pass completes most
+  // receivers from their hub rows: that won (2048-message shard round 4:
+  // 10.2 -> 6.6 ms) until the per-receiver kernel took done-neighbour and low
+  // in-degree receivers four per step (dnb_groups, gather_groups): N = 2
+  // slow rank's round 4 7.1 -> 4.7 ms, the other rank's 3.78 -> 0.95 ms with
+  // it off (profiles/r06_ab_w32_groups.txt)
+#ifndef GP_FLAT_ND
+#define GP_FLAT_ND 0
+#endif
+  const bool flat_nd = GP_FLAT_ND && W == 32 && c->cfg.flat_max_words > 0 && a.near_done &&
                        (double)c->prev_new_bits * 4.0 >= (double)c->n * (double)c->m;
-  const bool flat = W <= 32 && (W <= c->cfg.flat_max_words || flat_nd);
+  const bool flat = W <= 32 && (W <= c->cfg.flat_max_words || flat_nd) && !c->narrow_pr_now;
   const bool masked = !a.unfiltered && !flat && c->arc_mask_now;
   if (masked) {   // mask words of the owned vertices' in-arcs
     const int64_t kb = c->h_row_ptr[0] >> 6;
@@ -1621,9 +1887,9 @@ static void launch_expand_w(Ctx* c, ExpandArgs a) {
         else
           hipLaunchKernelGGL((k_expand<W, SCAN_FILTERED | SCAN_DPROBE>), grid, dim3(EBLOCK), 0, c->stream, a);
       }
-    } else if (W == 64 && mode == SCAN_UNFILTERED &&
+    } else if (W >= 8 && mode == SCAN_UNFILTERED &&
                ((GP_ALIAS_QUADS && a.alias) || (GP_NEAR_QUADS && a.near_done))) {   // (the first aliasing round)
-      if constexpr (W == 64)
+      if constexpr (W >= 8)
         hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED | SCAN_QUADS>), grid, dim3(EBLOCK), 0, c->stream, a);
     } else if (mode == SCAN_UNFILTERED) {
       hipLaunchKernelGGL((k_expand<W, SCAN_UNFILTERED>), grid, dim3(EBLOCK), 0, c->stream, a);

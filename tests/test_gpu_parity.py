@@ -830,7 +830,8 @@ def test_done_in_neighbours(pkg, oracle, m, flat_max_words):
     """Late early-exit rounds without liveness: a receiver whose first in-arcs
     (gather order, hubs first) come from a vertex that held its whole component
     at the end of the last round takes cmask & ~seen without gathering a row
-    (done_nb counts them; W = 64 two per wave-instruction, narrower rows in the
+    (done_nb counts them; W = 64 two or four per wave step, W = 32 four per
+    step, one per 16-lane group (dnb_groups), narrower rows in the
     per-receiver kernel's serial loop).  Bit-exact against the oracle,
     first-receipt matrix included."""
     rp, col = oracle.chung_lu(150_000, 12, 2.5, 41)
