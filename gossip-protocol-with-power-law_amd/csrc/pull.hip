@@ -141,6 +141,115 @@ __device__ __forceinline__ void pre_pairs(const ExpandArgs& a, LDS& L, u64 mp, i
   }
 }
 
+// The same four at a time (pre_quads; W = 64 without records): a
+// quarter-wave per receiver holds a whole 512-B row at 32 B per lane (words
+// 4ql .. 4ql + 3), and the receiver's seen row is loaded beside its staged
+// rows, one round trip per step instead of two (a receiver whose rows are all
+// zero has its seen row read for nothing: round 1's staged senders all send)
+#ifndef GP_PRE_QUADS
+#define GP_PRE_QUADS 1
+#endif
+#ifndef GP_PRE_QUADS_RIF
+#define GP_PRE_QUADS_RIF 1   // rows in flight per quarter-wave (2: 80 VGPRs, a wave per SIMD less, no faster)
+#endif
+template <int NG>
+__device__ __forceinline__ int take_group(u64& mq, int (&kq)[NG], int gq);
+template <class LDS>
+__device__ __forceinline__ void pre_quads(const ExpandArgs& a, LDS& L, u64 mq, int64_t base, uint32_t slot_of,
+                                          WaveStats& st) {
+  const int lane = threadIdx.x & 63, qd = lane >> 4, ql = lane & 15;
+  while (mq) {
+    int kq[4];
+    const int ks = take_group<4>(mq, kq, qd);
+    const bool on = ks >= 0;
+    const int64_t i = base + (on ? ks : 0);
+    const int v = (int)(a.vbegin + i);
+    const uint32_t sv_slot = (uint32_t)__shfl((int)slot_of, on ? ks : 0);
+    const int np = on ? (int)L.np[ks] : 0;
+    int nmax = 0;
+    uint32_t rows = 0, nsr = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int nq = __builtin_amdgcn_readlane(np, 16 * q);
+      const uint32_t sq = (uint32_t)__builtin_amdgcn_readlane((int)sv_slot, 16 * q);
+      nmax = max(nmax, nq);
+      rows += (uint32_t)nq;
+      nsr += (kq[q] >= 0 && sq != SLOT_NONE) ? 1u : 0u;
+    }
+    u64x2 s0 = {0, 0}, s1 = {0, 0}, c0 = {0, 0}, c1 = {0, 0};
+    if (on && sv_slot != SLOT_NONE) {
+      const u64* r = a.slot[sv_slot] + (size_t)v * 64 + 4 * ql;
+      s0 = *reinterpret_cast<const u64x2*>(r);
+      s1 = *reinterpret_cast<const u64x2*>(r + 2);
+    }
+    for (int q0 = 0; q0 < nmax; q0 += GP_PRE_QUADS_RIF) {
+      if (q0 < np) {   // (one branch per batch; past the last row a lane reloads it: same line, in flight)
+        u64x2 r0[GP_PRE_QUADS_RIF], r1[GP_PRE_QUADS_RIF];
+#pragma unroll
+        for (int q = 0; q < GP_PRE_QUADS_RIF; ++q) {
+          const u64* p = a.rows + (size_t)L.pre[ks][min(q0 + q, np - 1)] * 64 + 4 * ql;
+          r0[q] = *reinterpret_cast<const u64x2*>(p);
+          r1[q] = *reinterpret_cast<const u64x2*>(p + 2);
+        }
+#pragma unroll
+        for (int q = 0; q < GP_PRE_QUADS_RIF; ++q) {
+          c0 |= r0[q];
+          c1 |= r1[q];
+        }
+      }
+    }
+    st.add(S_GATHERED, (u64)rows);
+    st.add(S_ROW_BYTES, (u64)rows * 512ull);
+    st.add(S_SEEN_READ, nsr);
+    const u64x2 n0 = c0 & ~s0, n1 = c1 & ~s1;
+    uint32_t tot = (uint32_t)(__popcll(n0.x) + __popcll(n0.y) + __popcll(n1.x) + __popcll(n1.y));
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
+    u64 t = 0;
+    if (on && tot) {
+      u64* out = a.slot[a.wslot] + (size_t)v * 64 + 4 * ql;
+      *reinterpret_cast<u64x2*>(out) = s0 | n0;
+      *reinterpret_cast<u64x2*>(out + 2) = s1 | n1;
+      if (a.frx_next) {
+        u64* f = a.frx_next + (size_t)v * 64 + 4 * ql;
+        *reinterpret_cast<u64x2*>(f) = n0;
+        *reinterpret_cast<u64x2*>(f + 2) = n1;
+      }
+      const u64 nw[4] = {n0.x, n0.y, n1.x, n1.y};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!nw[j]) continue;
+        if (a.alive_next) atomicOr(&L.alive[4 * ql + j], nw[j]);   // (alive_add's words)
+        if (a.first) set_first_bytes(a.first + (size_t)i * (64 * 64), 4 * ql + j, nw[j], (uint32_t)a.rr);
+        if (a.digest) t ^= digest_term((uint32_t)a.rr, (uint32_t)(a.wbase + 4 * ql + j), nw[j]);
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) t ^= __shfl_xor(t, o);
+    uint32_t lmn = 0;   // lines of the new bits holding a nonzero word (lm_next; pair_finish)
+    if (a.lm_next) {
+      const uint32_t bq = (uint32_t)((__ballot(on && ((n0.x | n0.y | n1.x | n1.y) != 0ull)) >> (16 * qd)) & 0xFFFFull);
+#pragma unroll
+      for (int l = 0; l < 4; ++l) lmn |= ((bq >> (4 * l)) & 0xFu) ? (1u << l) : 0u;
+    }
+    if (ql == 0 && on && tot) {
+      L.tot[ks] = tot;
+      L.lmn[ks] = (uint8_t)lmn;
+      L.dig[ks] = t;
+    }
+    uint32_t nb = 0, nr = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t tq = (uint32_t)__builtin_amdgcn_readlane((int)tot, 16 * q);
+      nb += kq[q] >= 0 ? tq : 0u;
+      nr += (kq[q] >= 0 && tq) ? 1u : 0u;
+    }
+    st.add(S_NEW_BITS, nb);
+    st.add(S_RECEIVERS, nr);
+    st.add(S_WRITTEN, nr);
+  }
+}
+
 // Done in-neighbours (a.dbits rounds: early exit, no liveness,
 // one context).  Without liveness a receiver's new bits are OR_u seen(u) &
 // ~seen(v) over all its in-neighbours (ExpandArgs), and every Message-List is
@@ -844,7 +953,8 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
     if constexpr (W == 64 && (MODE & 3) == SCAN_PRE) {
       if (!ee) {   // prefiltered receivers two at a time, the rest below
         const u64 mp = m & __ballot(need && L.np[lane] != 0xFFu);
-        pre_pairs<W>(a, L, mp, base, slot_of, st);
+        if constexpr (GP_PRE_QUADS && !LDS_OF(MODE)::kCml) pre_quads(a, L, mp, base, slot_of, st);
+        else pre_pairs<W>(a, L, mp, base, slot_of, st);
         m &= ~mp;
       }
     } else if constexpr ((W == 32 || W == 16 || W == 8) && GP_PRE_GROUPS && (MODE & 3) == SCAN_PRE) {
