@@ -845,6 +845,26 @@ def test_done_in_neighbours(pkg, oracle, m, flat_max_words):
     r["eng"].close()
 
 
+@pytest.mark.parametrize("m", [1024, 512])
+@pytest.mark.parametrize("mode", [MODES[0], MODES[2]], ids=["pull", "pull-unfiltered"])
+def test_narrow_late_rounds_per_receiver(pkg, oracle, m, mode):
+    """W = 16 / 8 rows (the message shards of 4- and 8-GPU jobs) run on the
+    flat kernel, except the thin late rounds (under n*m/16 bits missing),
+    which take the per-receiver kernel with receivers in groups of 8 / 16
+    per wave step (dnb_groups, gather_groups): done-neighbour receivers can
+    only show up there.  Bit-exact against the oracle, first-receipt matrix
+    included."""
+    push_ratio, unfiltered_pct, _, arc_mask = mode
+    rp, col = oracle.chung_lu(150_000, 12, 2.5, 43)
+    g = pkg.CSR(150_000, rp, col, False)
+    origin = pkg.overlay.random_origins(g.n, m, seed=43)
+    r = _compare(pkg, oracle, g, origin, push_ratio=push_ratio, unfiltered_pct=unfiltered_pct,
+                 flat_max_words=16, arc_mask_permille=arc_mask)
+    dnb = [s["done_nb"] for s in r["stats"]]
+    assert sum(dnb) > 0, dnb
+    r["eng"].close()
+
+
 @pytest.mark.parametrize("hops", [1, 2, 3])
 def test_spread_keys_match_host(pkg, oracle, hops):
     """gp_spread_keys (device) equals overlay.spread_keys (host), u64-exact, on
