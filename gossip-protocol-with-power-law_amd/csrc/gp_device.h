@@ -398,11 +398,13 @@ enum ScanMode { SCAN_FILTERED = 0, SCAN_MASKED = 1, SCAN_UNFILTERED = 2, SCAN_PR
                 SCAN_LIST = 128 /* flag (k_expand, W >= 32, filtered / unfiltered): the waves take
                                    their receivers from a.ulist, the vertices that could still
                                    receive (late rounds), not 64 consecutive ids */,
-                SCAN_QUADS = 256 /* flag (k_expand, W = 64): done-neighbour receivers four per wave
-                                    step (dnb_quads) without the done probe, and (unfiltered, no
+                SCAN_QUADS = 256 /* flag (k_expand, unfiltered): W = 64: done-neighbour receivers
+                                    four per wave step (dnb_quads) without the done probe, and (no
                                     liveness) receivers of in-degree <= 32 two per step
                                     (gather_pairs): the first aliasing round, near-done pulls,
-                                    alive pulls from the half-held round */ };
+                                    alive pulls from the half-held round; W = 32 / 16 / 8
+                                    near-done pulls: low in-degree receivers 4 / 8 / 16 per step
+                                    (gather_groups) */ };
 
 // activity bits of arcs [j0, j0 + n) (n <= 64) from the per-arc mask, bit t =
 // arc j0 + t; j0 wave-uniform, so both words come in through scalar loads
