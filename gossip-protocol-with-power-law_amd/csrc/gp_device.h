@@ -259,8 +259,16 @@ constexpr double SUMMARY_RATIO = 256.0;
 #ifndef GP_ROWS_IN_FLIGHT_64
 #define GP_ROWS_IN_FLIGHT_64 3
 #endif
+// W = 8: the per-receiver kernel runs the 8-GPU job's thin late rounds
+// (narrow_pr_now); 2 rows in flight keep it at ~59 VGPRs against ~103 with 4
+// (N = 8 slowest rank 11.8 -> 11.3 ms, profiles/r06_ab_w8.txt)
+#ifndef GP_ROWS_IN_FLIGHT_NARROW
+#define GP_ROWS_IN_FLIGHT_NARROW 2
+#endif
 template <int W>
-struct RowsInFlight { static constexpr int value = W >= 64 ? GP_ROWS_IN_FLIGHT_64 : GP_ROWS_IN_FLIGHT; };
+struct RowsInFlight {
+  static constexpr int value = W >= 64 ? GP_ROWS_IN_FLIGHT_64 : W == 8 ? GP_ROWS_IN_FLIGHT_NARROW : GP_ROWS_IN_FLIGHT;
+};
 
 // per-wave LDS of the pull kernels; the mode-specific arrays take one element
 // when their mode is compiled out (LDS is what bounds the waves per CU)

@@ -777,8 +777,11 @@ __global__ EXPAND_BOUNDS __attribute__((amdgpu_waves_per_eu(1))) void k_expand(E
 #ifndef GP_GATHER_PAIRS
 #define GP_GATHER_PAIRS 1
 #endif
+#ifndef GP_GGROUPS_W8
+#define GP_GGROUPS_W8 0   // gather_groups at W = 8 too (16 receivers per step: 96 VGPRs, slower)
+#endif
   constexpr bool GPAIRS = GP_GATHER_PAIRS && W == 64 && QUADS && !ALIVE && SCAN == SCAN_UNFILTERED && !LIST;
-  constexpr bool GGROUPS = GP_GATHER_PAIRS && (W == 32 || W == 16 || W == 8) && QUADS && !ALIVE && SCAN == SCAN_UNFILTERED && !LIST;
+  constexpr bool GGROUPS = GP_GATHER_PAIRS && (W == 32 || W == 16 || (W == 8 && GP_GGROUPS_W8)) && QUADS && !ALIVE && SCAN == SCAN_UNFILTERED && !LIST;
   WaveStats st;
   ws_zero<EWAVES>(st);
   const int64_t base = ((int64_t)blockIdx.x * EWAVES + wib) * 64;
