@@ -572,15 +572,20 @@ __device__ __forceinline__ void pre_groups(const ExpandArgs& a, LDS& L, u64 mp, 
   }
 }
 
-// rows in flight per receiver of gather_groups / gather_pairs
+// rows in flight per receiver of gather_pairs (W = 64: 2, 72 VGPRs, 7 waves
+// per SIMD; 3 took 76 and 6 waves: C4 round 4 6.70-6.74 -> 6.44-6.48 ms with
+// 2) and of gather_groups (W = 32: 3; 2 was slower, profiles/r06_ab_grif.txt)
 #ifndef GP_GPAIR_RIF
-#define GP_GPAIR_RIF 3
+#define GP_GPAIR_RIF 2
+#endif
+#ifndef GP_GGROUP_RIF
+#define GP_GGROUP_RIF 3
 #endif
 
 // W = 32 near-done unfiltered pulls: receivers of in-degree <= 16 four per
 // wave step, one per 16-lane group (gather_pairs' scheme at a 256-B row per
 // group-instruction): column ids, seen and component rows in one round trip,
-// then GP_GPAIR_RIF rows per group in flight until the target is covered.
+// then GP_GGROUP_RIF rows per group in flight until the target is covered.
 template <int W, class LDS>
 __device__ __forceinline__ void gather_groups(const ExpandArgs& a, LDS& L, u64 mp, int64_t base, uint32_t slot_of,
                                               WaveStats& st) {
@@ -615,21 +620,21 @@ __device__ __forceinline__ void gather_groups(const ExpandArgs& a, LDS& L, u64 m
     bool live = on && (!ee || (want.x | want.y) != 0ull);
     u64x2 acc = {0, 0};
     u64 rows = 0, pieces = 0;
-    for (int k0 = 0; k0 < dmax; k0 += GP_GPAIR_RIF) {
+    for (int k0 = 0; k0 < dmax; k0 += GP_GGROUP_RIF) {
       const u64 lb = __ballot(live);
       if (lb == 0ull) break;
       if (live && k0 < deg) {   // (one branch per batch, gather_pairs)
-        u64x2 r[GP_GPAIR_RIF];
+        u64x2 r[GP_GGROUP_RIF];
 #pragma unroll
-        for (int q = 0; q < GP_GPAIR_RIF; ++q) r[q] = load_piece<W>(a.rows, L.idx[LG * gq + min(k0 + q, deg - 1)], lw);
+        for (int q = 0; q < GP_GGROUP_RIF; ++q) r[q] = load_piece<W>(a.rows, L.idx[LG * gq + min(k0 + q, deg - 1)], lw);
 #pragma unroll
-        for (int q = 0; q < GP_GPAIR_RIF; ++q) acc |= r[q];
+        for (int q = 0; q < GP_GGROUP_RIF; ++q) acc |= r[q];
       }
 #pragma unroll
-      for (int q = 0; q < GP_GPAIR_RIF; ++q) pieces += line_pieces<W>(__ballot(live && k0 + q < deg));
+      for (int q = 0; q < GP_GGROUP_RIF; ++q) pieces += line_pieces<W>(__ballot(live && k0 + q < deg));
 #pragma unroll
       for (int q = 0; q < NG; ++q)
-        if ((lb >> (LG * q)) & ((1ull << LG) - 1ull)) rows += (u64)min(GP_GPAIR_RIF, max(dq[q] - k0, 0));
+        if ((lb >> (LG * q)) & ((1ull << LG) - 1ull)) rows += (u64)min(GP_GGROUP_RIF, max(dq[q] - k0, 0));
       if (ee) {
         const u64x2 miss = want & ~acc;
         live = live && (miss.x | miss.y) != 0ull;
